@@ -1,0 +1,376 @@
+// api.cpp — the C ABI (include/rt_api.h): scene upload, frame render, tile
+// partition, ray queries.  Replaces generate_image (main.rs:85-114) and the
+// scene construction behind it (scene.rs:180-223).  Errors become return codes
+// (the reference panics).
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_api.h"
+#include "api_internal.h"
+#include "render.h"
+#include "rt_device.h"
+#include "scene_build.h"
+
+namespace rt {
+
+static thread_local std::string g_last_error;
+
+int set_error(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+}  // namespace rt
+
+using namespace rt;
+
+#define HIP_TRY(expr)                                                                         \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess)                                                                 \
+            return set_error(e_ == hipErrorOutOfMemory ? RT_ERR_NOMEM : RT_ERR_DEVICE,        \
+                             std::string(#expr) + ": " + hipGetErrorString(e_));              \
+    } while (0)
+
+struct rt_scene {
+    int device = 0;
+    DevScene dev{};
+    std::vector<void*> allocs;
+    rt_scene_info info{};
+    // spill workspace for the traversal stack (grown on demand)
+    uint32_t* spill_n = nullptr;
+    double* spill_t = nullptr;
+    size_t spill_entries = 0;
+    unsigned long long* d_stats = nullptr;
+};
+
+namespace {
+
+template <class T>
+int upload(rt_scene* s, const std::vector<T>& v, const T** out) {
+    *out = nullptr;
+    if (v.empty()) return RT_OK;
+    void* p = nullptr;
+    HIP_TRY(hipMalloc(&p, v.size() * sizeof(T)));
+    s->allocs.push_back(p);
+    HIP_TRY(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    s->info.device_bytes += v.size() * sizeof(T);
+    *out = (const T*)p;
+    return RT_OK;
+}
+
+int upload_bvh(rt_scene* s, const HostBvhArrays& h, DevBvh& d) {
+    int rc;
+    std::memset(&d, 0, sizeof(d));
+    if ((rc = upload(s, h.nodes, &d.nodes))) return rc;
+    store3(d.root_min, h.root.min);
+    store3(d.root_max, h.root.max);
+    d.n_prims = h.n_prims;
+    d.depth = h.depth;
+    if ((rc = upload(s, h.shapes, &d.shapes))) return rc;
+    if ((rc = upload(s, h.tris, &d.tris))) return rc;
+    if ((rc = upload(s, h.tri_cold, &d.tri_cold))) return rc;
+    if ((rc = upload(s, h.tri_inv_area, &d.tri_inv_area))) return rc;
+    if ((rc = upload(s, h.mat, &d.mat))) return rc;
+    if ((rc = upload(s, h.gid, &d.gid))) return rc;
+    return RT_OK;
+}
+
+void free_scene(rt_scene* s) {
+    if (!s) return;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(s->device);
+    for (void* p : s->allocs) (void)hipFree(p);
+    if (s->spill_n) (void)hipFree(s->spill_n);
+    if (s->spill_t) (void)hipFree(s->spill_t);
+    if (s->d_stats) (void)hipFree(s->d_stats);
+    (void)hipSetDevice(cur);
+    delete s;
+}
+
+int check_params(const rt_render_params* p) {
+    if (!p) return set_error(RT_ERR_INVALID, "params is NULL");
+    if (p->width == 0 || p->height == 0) return set_error(RT_ERR_INVALID, "width/height must be > 0");
+    if (p->spp == 0) return set_error(RT_ERR_INVALID, "spp must be > 0");
+    if (p->ray_depth > 255) return set_error(RT_ERR_INVALID, "ray_depth is a u8 in the reference (scene.rs:85)");
+    if (p->fov_axis != RT_FOV_X && p->fov_axis != RT_FOV_Y) return set_error(RT_ERR_INVALID, "bad fov_axis");
+    return RT_OK;
+}
+
+// Camera::new (camera.rs:17-46) on the host + the tile map of one rank.
+KParams make_kparams(const rt_render_params* p, uint32_t rank, uint32_t world) {
+    KParams k;
+    std::memset(&k, 0, sizeof(k));
+    k.width = p->width; k.height = p->height; k.spp = p->spp; k.ray_depth = p->ray_depth;
+    k.fw = (double)p->width; k.fh = (double)p->height;
+    if (p->fov_axis == RT_FOV_Y) {
+        k.tan_y = std::tan(p->fov / 2.0);
+        double aspect = k.fh / k.fw;
+        k.tan_x = k.tan_y / aspect;
+    } else {
+        k.tan_x = std::tan(p->fov / 2.0);
+        double aspect = k.fw / k.fh;
+        k.tan_y = k.tan_x / aspect;
+    }
+    for (int i = 0; i < 3; ++i) {
+        k.cam_pos[i] = p->cam_position[i]; k.cam_right[i] = p->cam_right[i];
+        k.cam_up[i] = p->cam_up[i]; k.cam_fwd[i] = p->cam_forward[i]; k.bg[i] = p->bg_color[i];
+    }
+    k.scale01 = inclusive_scale(0.0, 1.0);
+    k.scale11 = inclusive_scale(-1.0, 1.0);
+    k.seed = p->seed;
+    k.rank = rank; k.world = world;
+    k.tiles_x = (p->width + RT_TILE - 1) / RT_TILE;
+    k.tiles_y = (p->height + RT_TILE - 1) / RT_TILE;
+    k.n_tiles = (uint64_t)k.tiles_x * k.tiles_y;
+    return k;
+}
+
+uint32_t slots_per_rank(const KParams& k) { return (uint32_t)((k.n_tiles + k.world - 1) / k.world); }
+
+// Spill area for stack entries beyond the LDS short stack: depth bound of the
+// deepest BVH, one slot per launched lane.
+int ensure_spill(rt_scene* s, uint64_t lanes) {
+    uint32_t depth = s->dev.max_depth;
+    if (depth <= (uint32_t)kMaxBvhDepthShort) return RT_OK;
+    size_t need = (size_t)(depth - kMaxBvhDepthShort) * lanes;
+    if (need <= s->spill_entries) return RT_OK;
+    if (s->spill_n) (void)hipFree(s->spill_n);
+    if (s->spill_t) (void)hipFree(s->spill_t);
+    s->spill_n = nullptr; s->spill_t = nullptr; s->spill_entries = 0;
+    HIP_TRY(hipMalloc(&s->spill_n, need * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc(&s->spill_t, need * sizeof(double)));
+    s->spill_entries = need;
+    return RT_OK;
+}
+
+template <class T>
+struct DevBuf {  // RAII device buffer for per-call scratch
+    T* p = nullptr;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+    hipError_t alloc(size_t n) { return hipMalloc((void**)&p, (n ? n : 1) * sizeof(T)); }
+};
+
+}  // namespace
+
+extern "C" {
+
+const char* rt_last_error(void) { return g_last_error.c_str(); }
+int rt_api_version(void) { return RT_API_VERSION; }
+int rt_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int rt_scene_create(const rt_scene_desc* desc, rt_scene** out) {
+    if (!desc || !out) return set_error(RT_ERR_INVALID, "desc/out is NULL");
+    *out = nullptr;
+    HostScene hs;
+    std::string err = build_scene(*desc, hs);
+    if (!err.empty()) return set_error(RT_ERR_INVALID, err);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return set_error(RT_ERR_DEVICE, "no HIP device visible (the hot path has no CPU fallback)");
+    rt_scene* s = new rt_scene();
+    HIP_TRY(hipGetDevice(&s->device));
+    auto t0 = std::chrono::steady_clock::now();
+    int rc = RT_OK;
+    DevScene& d = s->dev;
+    d.n_planes = (uint32_t)hs.planes.size();
+    if ((rc = upload(s, hs.planes, &d.planes)) || (rc = upload(s, hs.plane_mat, &d.plane_mat)) ||
+        (rc = upload(s, hs.plane_gid, &d.plane_gid)) || (rc = upload(s, hs.mats, &d.mats)) ||
+        (rc = upload_bvh(s, hs.bvh[0], d.boxes)) || (rc = upload_bvh(s, hs.bvh[1], d.ells)) ||
+        (rc = upload_bvh(s, hs.bvh[2], d.tris)) || (rc = upload_bvh(s, hs.bvh[3], d.lboxes)) ||
+        (rc = upload_bvh(s, hs.bvh[4], d.lells)) || (rc = upload_bvh(s, hs.bvh[5], d.ltris))) {
+        free_scene(s);
+        return rc;
+    }
+    d.n_lights = d.lboxes.n_prims + d.lells.n_prims + d.ltris.n_prims;
+    d.max_depth = 0;
+    const DevBvh* all[6] = {&d.boxes, &d.ells, &d.tris, &d.lboxes, &d.lells, &d.ltris};
+    for (int k = 0; k < 6; ++k) {
+        d.max_depth = std::max(d.max_depth, all[k]->depth);
+        s->info.bvh_nodes[k] = hs.bvh[k].nodes.size();
+        s->info.bvh_depth[k] = hs.bvh[k].depth;
+    }
+    HIP_TRY(hipMalloc(&s->d_stats, 8 * sizeof(unsigned long long)));
+    s->info.n_planes = d.n_planes;
+    s->info.n_boxes = d.boxes.n_prims;
+    s->info.n_ellipsoids = d.ells.n_prims;
+    s->info.n_triangles = d.tris.n_prims;
+    s->info.n_light_boxes = d.lboxes.n_prims;
+    s->info.n_light_ellipsoids = d.lells.n_prims;
+    s->info.n_light_triangles = d.ltris.n_prims;
+    s->info.build_ms = hs.build_ms;
+    s->info.upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    *out = s;
+    return RT_OK;
+}
+
+void rt_scene_destroy(rt_scene* s) { free_scene(s); }
+
+int rt_scene_get_info(const rt_scene* s, rt_scene_info* out) {
+    if (!s || !out) return set_error(RT_ERR_INVALID, "scene/out is NULL");
+    *out = s->info;
+    return RT_OK;
+}
+
+int rt_tiles_per_rank(const rt_render_params* p, uint32_t world, uint32_t* n) {
+    int rc = check_params(p);
+    if (rc) return rc;
+    if (world == 0 || !n) return set_error(RT_ERR_INVALID, "world must be > 0");
+    *n = slots_per_rank(make_kparams(p, 0, world));
+    return RT_OK;
+}
+
+int rt_render_tiles_async(rt_scene* s, const rt_render_params* p, uint32_t rank, uint32_t world,
+                          double* d_tile_rgb, void* stream) {
+    int rc = check_params(p);
+    if (rc) return rc;
+    if (!s || !d_tile_rgb) return set_error(RT_ERR_INVALID, "scene/output is NULL");
+    if (world == 0 || rank >= world) return set_error(RT_ERR_INVALID, "rank must be < world");
+    KParams k = make_kparams(p, rank, world);
+    uint32_t slots = slots_per_rank(k);
+    if ((rc = ensure_spill(s, (uint64_t)slots * 256))) return rc;
+    HIP_TRY(launch_path(s->dev, k, slots, d_tile_rgb, nullptr, nullptr, s->spill_n, s->spill_t,
+                        (hipStream_t)stream));
+    return RT_OK;
+}
+
+int rt_unpack_tiles_async(const rt_render_params* p, uint32_t world, const double* d_gathered, double* d_image,
+                          void* stream) {
+    int rc = check_params(p);
+    if (rc) return rc;
+    if (!d_gathered || !d_image || world == 0) return set_error(RT_ERR_INVALID, "bad unpack arguments");
+    KParams k = make_kparams(p, 0, world);
+    HIP_TRY(launch_unpack(d_gathered, d_image, p->width, p->height, k.tiles_x, world, slots_per_rank(k),
+                          (hipStream_t)stream));
+    return RT_OK;
+}
+
+int rt_render(rt_scene* s, const rt_render_params* p, double* out_mean_rgb, int32_t* opt_hit_ids,
+              rt_stats* opt_stats) {
+    auto t0 = std::chrono::steady_clock::now();
+    int rc = check_params(p);
+    if (rc) return rc;
+    if (!s || !out_mean_rgb) return set_error(RT_ERR_INVALID, "scene/output is NULL");
+    HIP_TRY(hipSetDevice(s->device));
+    KParams k = make_kparams(p, 0, 1);
+    const uint32_t slots = slots_per_rank(k);
+    const uint64_t npx = (uint64_t)p->width * p->height;
+    const bool want_hits = opt_hit_ids && (p->flags & RT_FLAG_HIT_IDS);
+    const bool want_stats = opt_stats && (p->flags & RT_FLAG_STATS);
+    if ((rc = ensure_spill(s, (uint64_t)slots * 256))) return rc;
+    DevBuf<double> tiles, img;
+    DevBuf<int32_t> hits;
+    HIP_TRY(tiles.alloc((size_t)slots * 256 * 3));
+    HIP_TRY(img.alloc(npx * 3));
+    const uint64_t nhits = npx * p->spp * p->ray_depth;
+    if (want_hits) HIP_TRY(hits.alloc(nhits));
+    if (want_stats) HIP_TRY(hipMemset(s->d_stats, 0, 8 * sizeof(unsigned long long)));
+    hipEvent_t e0, e1;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    HIP_TRY(hipEventRecord(e0, 0));
+    hipError_t le = launch_path(s->dev, k, slots, tiles.p, want_hits ? hits.p : nullptr,
+                                want_stats ? s->d_stats : nullptr, s->spill_n, s->spill_t, 0);
+    HIP_TRY(hipEventRecord(e1, 0));
+    if (le != hipSuccess) {
+        (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
+        return set_error(RT_ERR_DEVICE, std::string("path kernel launch: ") + hipGetErrorString(le));
+    }
+    HIP_TRY(launch_unpack(tiles.p, img.p, p->width, p->height, k.tiles_x, 1, slots, 0));
+    HIP_TRY(hipDeviceSynchronize());
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    HIP_TRY(hipMemcpy(out_mean_rgb, img.p, npx * 3 * sizeof(double), hipMemcpyDeviceToHost));
+    if (want_hits) HIP_TRY(hipMemcpy(opt_hit_ids, hits.p, nhits * sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (opt_stats) {
+        std::memset(opt_stats, 0, sizeof(*opt_stats));
+        if (want_stats) {
+            unsigned long long c[8];
+            HIP_TRY(hipMemcpy(c, s->d_stats, sizeof(c), hipMemcpyDeviceToHost));
+            opt_stats->paths = c[0]; opt_stats->segments = c[1]; opt_stats->aabb_tests = c[2];
+            opt_stats->tri_tests = c[3]; opt_stats->shape_tests = c[4]; opt_stats->shaded_hits = c[5];
+            opt_stats->light_queries = c[6]; opt_stats->light_hits = c[7];
+        }
+        opt_stats->kernel_ms = ms;
+        opt_stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return RT_OK;
+}
+
+int rt_intersect_rays(rt_scene* s, const double* rays, uint32_t n, rt_hit* out) {
+    if (!s || (!rays && n) || (!out && n)) return set_error(RT_ERR_INVALID, "bad arguments");
+    if (n == 0) return RT_OK;
+    HIP_TRY(hipSetDevice(s->device));
+    int rc = ensure_spill(s, ((uint64_t)n + 255) / 256 * 256);
+    if (rc) return rc;
+    DevBuf<double> r;
+    DevBuf<rt_hit> h;
+    HIP_TRY(r.alloc((size_t)n * 6));
+    HIP_TRY(h.alloc(n));
+    HIP_TRY(hipMemcpy(r.p, rays, (size_t)n * 6 * sizeof(double), hipMemcpyHostToDevice));
+    HIP_TRY(launch_intersect(s->dev, r.p, n, h.p, s->spill_n, s->spill_t, 0));
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(out, h.p, (size_t)n * sizeof(rt_hit), hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+static int light_query(rt_scene* s, const double* rays, uint32_t n, int mode, double* out, uint32_t* cnt) {
+    if (!s || (!rays && n) || (!out && n)) return set_error(RT_ERR_INVALID, "bad arguments");
+    if (n == 0) return RT_OK;
+    HIP_TRY(hipSetDevice(s->device));
+    int rc = ensure_spill(s, ((uint64_t)n + 255) / 256 * 256);
+    if (rc) return rc;
+    DevBuf<double> r, o;
+    DevBuf<uint32_t> c;
+    HIP_TRY(r.alloc((size_t)n * 6));
+    HIP_TRY(o.alloc(n));
+    if (cnt) HIP_TRY(c.alloc(n));
+    HIP_TRY(hipMemcpy(r.p, rays, (size_t)n * 6 * sizeof(double), hipMemcpyHostToDevice));
+    HIP_TRY(launch_light(s->dev, r.p, n, mode, o.p, cnt ? c.p : nullptr, s->spill_n, s->spill_t, 0));
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(out, o.p, (size_t)n * sizeof(double), hipMemcpyDeviceToHost));
+    if (cnt) HIP_TRY(hipMemcpy(cnt, c.p, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+int rt_light_pdf_rays(rt_scene* s, const double* pos_dir, uint32_t n, double* out_pdf) {
+    return light_query(s, pos_dir, n, 1, out_pdf, nullptr);
+}
+
+// Extra query (not in the reference's call graph as a batch): the raw
+// intersect_lights accumulation of Light::pdf without the epsilon offset and
+// the 1/len normalisation, plus the number of callbacks.  Used by the
+// triangle::aaa known-answer test (primitives/triangle.rs:98-128).
+int rt_intersect_lights_rays(rt_scene* s, const double* rays, uint32_t n, double* out_impact, uint32_t* out_count) {
+    return light_query(s, rays, n, 0, out_impact, out_count);
+}
+
+// Diagnostic: device f64 sqrt (op 0) / division (op 1) for bit-exactness checks.
+int rt_probe_fp64(int op, const double* a, const double* b, uint32_t n, double* out) {
+    if (!a || !out || (op == 1 && !b) || op < 0 || op > 1) return set_error(RT_ERR_INVALID, "bad arguments");
+    if (n == 0) return RT_OK;
+    DevBuf<double> da, db, dout;
+    HIP_TRY(da.alloc(n));
+    HIP_TRY(db.alloc(n));
+    HIP_TRY(dout.alloc(n));
+    HIP_TRY(hipMemcpy(da.p, a, n * sizeof(double), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(db.p, op == 1 ? b : a, n * sizeof(double), hipMemcpyHostToDevice));
+    HIP_TRY(launch_fp64_probe(da.p, db.p, dout.p, n, op, 0));
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(out, dout.p, n * sizeof(double), hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+}  // extern "C"

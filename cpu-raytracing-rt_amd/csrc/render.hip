@@ -1,0 +1,629 @@
+// render.hip — MI355X (gfx950) kernels of the path-tracing hot path.
+//
+//   path_kernel          generate_image pixel loop (main.rs:94-103) fused with
+//                        Camera::fuzzy_ray (camera.rs:48-55) and raytrace /
+//                        raytrace_impl (raytrace.rs:8-60) in throughput form.
+//                        One lane = one pixel; the lane walks its spp samples
+//                        in order (deterministic per-pixel sum) and regenerates
+//                        a camera path as soon as one ends, so lanes whose paths
+//                        are short do not idle while a neighbour finishes.
+//   intersect_kernel     batch `intersect` (intersections.rs:42-62)
+//   light_kernel         batch intersect_lights / Light::pdf
+//                        (intersections.rs:87-91, ray_sampler.rs:132-139)
+//   unpack_kernel        gathered tiles -> row-major image
+//
+// BVH traversal keeps the reference's exact visit order (bvh.rs:151-210): the
+// far child goes on a per-lane stack (short part in LDS, overflow in a global
+// spill area sized from the deepest BVH) with its clamped entry t, and is
+// re-checked against the updated best when popped — identical to the
+// recursive "visit near, then far if still < best".
+#include <hip/hip_runtime.h>
+
+#include "render.h"
+#include "rt_device.h"
+
+namespace rt {
+
+constexpr int kBlock = 256;
+constexpr int kShort = kMaxBvhDepthShort;
+
+// ---------------------------------------------------------------- stack ---
+struct Stack {
+    uint32_t* sn;        // LDS node slots, stride kBlock
+    double* st;          // LDS entry-t slots, stride kBlock
+    uint32_t* gn;        // global spill (stride = spill_stride) or null
+    double* gt;
+    uint32_t stride;
+    int sp;
+    RT_D void push(uint32_t node, double t) {
+        if (sp < kShort) { sn[sp * kBlock] = node; st[sp * kBlock] = t; }
+        else { gn[(size_t)(sp - kShort) * stride] = node; gt[(size_t)(sp - kShort) * stride] = t; }
+        ++sp;
+    }
+    RT_D void pop(uint32_t& node, double& t) {
+        --sp;
+        if (sp < kShort) { node = sn[sp * kBlock]; t = st[sp * kBlock]; }
+        else { node = gn[(size_t)(sp - kShort) * stride]; t = gt[(size_t)(sp - kShort) * stride]; }
+    }
+};
+
+// Best candidate of one query: materialised into a Hit only for the winner.
+struct Cand {
+    double t;
+    double u, v;       // triangle barycentrics
+    uint32_t prim;     // index in its list / BVH order
+    uint32_t aux;      // shape face / plane side bits
+    uint32_t kind;     // 0 plane, 1 box, 2 ellipsoid, 3 triangle
+    bool valid;
+};
+
+// closest hit of one shape in model space; t + aux
+template <int KIND>
+RT_D bool shape_closest(const DevShape& s, V3 o, V3 d, double& t, uint32_t& aux) {
+    V3 mo, md;
+    model_ray(s, o, d, mo, md);
+    if (KIND == 0) return plane_t(load3(s.shape), mo, md, t, aux);
+    if (KIND == 1) {
+        Bpi en, ex;
+        int k = box_coef(load3(s.shape), mo, md, en, ex);
+        if (k == 2) { t = en.t; aux = bpi_aux(en, false); return true; }
+        if (k == 1) { t = ex.t; aux = bpi_aux(ex, true); return true; }
+        return false;
+    }
+    double t1, t2;
+    int k = ell_coef(load3(s.shape), mo, md, t1, t2);
+    if (k == 2) { t = t1; aux = 0; return true; }
+    if (k == 1) { t = t2; aux = 8; return true; }
+    return false;
+}
+
+// BVH::intersection (bvh.rs:27-36) + Node::intersection (bvh.rs:151-186)
+template <int KIND, bool ST>
+RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, Stack& S, Cnt<ST>& C, double& bt_out, double& bu,
+                      double& bv, uint32_t& bprim, uint32_t& baux) {
+    if (B.n_prims == 0) return false;
+    double t0;
+    C.aabb();
+    if (!aabb_hit(load3(B.root_min), load3(B.root_max), o, d, t0)) return false;
+    bool valid = false;
+    double best = INFINITY;
+    uint32_t node = 0;
+    S.sp = 0;
+    for (;;) {
+        const DevNode& n = B.nodes[node];
+        const uint32_t cnt = n.count, start = n.start;
+        for (uint32_t i = start; i < start + cnt; ++i) {
+            double t, u = 0.0, v = 0.0;
+            uint32_t aux = 0;
+            bool h;
+            if (KIND == 3) { C.tri(); h = tri_uvt(B.tris[i], o, d, u, v, t); }
+            else { C.shape(); h = shape_closest<KIND>(B.shapes[i], o, d, t, aux); }
+            if (h && (!valid || t < best)) {  // update_best_intersection (bvh.rs:213-222)
+                valid = true; best = t; bu = u; bv = v; bprim = i; baux = aux;
+            }
+        }
+        const int32_t left = n.left;
+        if (left >= 0) {
+            double lt = 0.0, rt2 = 0.0;
+            C.aabb(2);
+            bool lh = aabb_hit(load3(n.lmin), load3(n.lmax), o, d, lt);
+            bool rh = aabb_hit(load3(n.rmin), load3(n.rmax), o, d, rt2);
+            const double bt = best;  // +inf when no hit yet
+            const double li = lh ? (lt < bt ? lt : bt) : bt;
+            const double ri = rh ? (rt2 < bt ? rt2 : bt) : bt;
+            if (li < bt) {
+                if (ri < bt) {
+                    if (li < ri) { S.push((uint32_t)n.right, ri); node = (uint32_t)left; }
+                    else { S.push((uint32_t)left, li); node = (uint32_t)n.right; }
+                } else node = (uint32_t)left;
+                continue;
+            } else if (ri < bt) { node = (uint32_t)n.right; continue; }
+        }
+        bool found = false;
+        while (S.sp > 0) {
+            uint32_t nn; double tt;
+            S.pop(nn, tt);
+            if (tt < best) { node = nn; found = true; break; }
+        }
+        if (!found) break;
+    }
+    if (valid) bt_out = best;
+    return valid;
+}
+
+// Materialise the winning candidate (model-space normals) + its rotation.
+RT_D Hit materialise(const DevScene& S, const Cand& c, V3 o, V3 d, Quat& rot, uint32_t& mat, int32_t& gid) {
+    Hit h;
+    h.t = c.t;
+    if (c.kind == 3) {  // Triangle::intersection tail (triangle.rs:71-79), DONT_ROTATE
+        const DevBvh& B = S.tris;
+        const DevTriCold& tc = B.tri_cold[c.prim];
+        V3 n = load3(tc.ng), na = load3(tc.na), nb = load3(tc.nb), nc = load3(tc.nc);
+        V3 sn = normalize(na + (nb - na) * c.u + (nc - na) * c.v);
+        bool inside = dot(d, n) > 0.0;
+        h.ng = inside ? -n : n;
+        h.ns = inside ? -sn : sn;
+        h.inside = inside;
+        rot = Quat{1.0, v3(0.0, 0.0, 0.0)};
+        mat = B.mat[c.prim];
+        gid = B.gid[c.prim];
+        return h;
+    }
+    const DevShape* sp;
+    if (c.kind == 0) { sp = &S.planes[c.prim]; mat = S.plane_mat[c.prim]; gid = S.plane_gid[c.prim]; }
+    else {
+        const DevBvh& B = c.kind == 1 ? S.boxes : S.ells;
+        sp = &B.shapes[c.prim]; mat = B.mat[c.prim]; gid = B.gid[c.prim];
+    }
+    const DevShape s = *sp;
+    rot = load_quat(s.rot);
+    if (c.kind == 0) {
+        V3 n = load3(s.shape) * ((c.aux & 1u) ? 1.0 : -1.0);
+        h.ng = n; h.ns = n; h.inside = false;
+    } else if (c.kind == 1) {
+        V3 n = aux_box_normal(c.aux);
+        h.ng = n; h.ns = n; h.inside = (c.aux & 8u) != 0;
+    } else {
+        V3 mo, md;
+        model_ray(s, o, d, mo, md);
+        V3 n = ell_normal(load3(s.shape), mo, md, c.t);
+        bool inside = (c.aux & 8u) != 0;
+        if (inside) n = -n;
+        h.ng = n; h.ns = n; h.inside = inside;
+    }
+    return h;
+}
+
+// intersect(ray, &scene.primitives, +inf) (intersections.rs:42-62)
+template <bool ST>
+RT_D bool scene_intersect(const DevScene& S, V3 o, V3 d, Stack& stk, Cnt<ST>& C, Hit& out, uint32_t& mat,
+                          int32_t& gid) {
+    Cand best;
+    best.valid = false; best.t = 0.0; best.u = best.v = 0.0; best.prim = 0; best.aux = 0; best.kind = 0;
+    for (uint32_t i = 0; i < S.n_planes; ++i) {  // :45-49
+        double t; uint32_t aux;
+        C.shape();
+        if (!shape_closest<0>(S.planes[i], o, d, t, aux)) continue;
+        if (!best.valid || t < best.t) { best.valid = true; best.t = t; best.prim = i; best.aux = aux; best.kind = 0; }
+    }
+    {
+        double t, u, v; uint32_t p, aux = 0;
+        if (bvh_closest<1, ST>(S.boxes, o, d, stk, C, t, u, v, p, aux) && (!best.valid || t < best.t)) {
+            best.valid = true; best.t = t; best.prim = p; best.aux = aux; best.kind = 1;
+        }
+    }
+    {
+        double t, u, v; uint32_t p, aux = 0;
+        if (bvh_closest<2, ST>(S.ells, o, d, stk, C, t, u, v, p, aux) && (!best.valid || t < best.t)) {
+            best.valid = true; best.t = t; best.prim = p; best.aux = aux; best.kind = 2;
+        }
+    }
+    {
+        double t, u = 0.0, v = 0.0; uint32_t p, aux = 0;
+        if (bvh_closest<3, ST>(S.tris, o, d, stk, C, t, u, v, p, aux) && (!best.valid || t < best.t)) {
+            best.valid = true; best.t = t; best.prim = p; best.u = u; best.v = v; best.aux = 0; best.kind = 3;
+        }
+    }
+    if (!best.valid) return false;
+    if (!(best.t * magnitude(d) <= INFINITY)) return false;  // :56
+    Quat rot;
+    Hit h = materialise(S, best, o, d, rot, mat, gid);
+    out = rotated(h, rot);
+    C.shaded();
+    return true;
+}
+
+// ---------------------------------------------------------- light pdf ----
+// intersection_probability.rs:9-35 + to_direction_probability (ray_sampler.rs:172-174)
+RT_D double prob_box(V3 s) { return 1.0 / ((s.y * s.z + s.x * s.z) + s.x * s.y) / 8.0; }
+RT_D double prob_ell(V3 r, V3 ng) {
+    V3 coef = mul(v3(r.y * r.z, r.x * r.z, r.x * r.y), ng);
+    return 1.0 / (4.0 * kPi * sqrt(dot(coef, coef)));
+}
+
+// Node::intersections (bvh.rs:188-210) accumulating the Light::pdf callback
+template <int KIND, bool ST>
+RT_D void bvh_all(const DevBvh& B, V3 o, V3 d, Stack& S, Cnt<ST>& C, double& impact, uint32_t& nhits) {
+    if (B.n_prims == 0) return;
+    double t0;
+    C.aabb();
+    if (!aabb_hit(load3(B.root_min), load3(B.root_max), o, d, t0)) return;
+    uint32_t node = 0;
+    S.sp = 0;
+    for (;;) {
+        const DevNode& n = B.nodes[node];
+        const uint32_t cnt = n.count, start = n.start;
+        for (uint32_t i = start; i < start + cnt; ++i) {
+            if (KIND == 3) {
+                C.tri();
+                double u, v, t;
+                if (tri_uvt(B.tris[i], o, d, u, v, t)) {
+                    V3 ng = load3(B.tri_cold[i].ng);  // sign flip (triangle.rs:76) cancels in |d.n|
+                    impact += B.tri_inv_area[i] * (t * t / fabs(dot(d, ng)));
+                    C.lhit(); nhits++;
+                }
+            } else {
+                C.shape();
+                const DevShape s = B.shapes[i];
+                V3 mo, md;
+                model_ray(s, o, d, mo, md);
+                Quat q = load_quat(s.rot);
+                V3 sz = load3(s.shape);
+                if (KIND == 1) {
+                    Bpi en, ex;
+                    int k = box_coef(sz, mo, md, en, ex);
+                    const double pb = prob_box(sz);
+                    if (k == 2) {
+                        V3 ng = normalize(rotate(q, bpi_normal(en)));
+                        impact += pb * (en.t * en.t / fabs(dot(d, ng)));
+                        C.lhit(); nhits++;
+                    }
+                    if (k >= 1) {
+                        V3 ng = normalize(rotate(q, bpi_normal(ex)));
+                        impact += pb * (ex.t * ex.t / fabs(dot(d, ng)));
+                        C.lhit(); nhits++;
+                    }
+                } else {
+                    double t1, t2;
+                    int k = ell_coef(sz, mo, md, t1, t2);
+                    if (k == 2) {
+                        V3 ng = normalize(rotate(q, ell_normal(sz, mo, md, t1)));
+                        impact += prob_ell(sz, ng) * (t1 * t1 / fabs(dot(d, ng)));
+                        C.lhit(); nhits++;
+                    }
+                    if (k >= 1) {
+                        V3 ng = normalize(rotate(q, -ell_normal(sz, mo, md, t2)));
+                        impact += prob_ell(sz, ng) * (t2 * t2 / fabs(dot(d, ng)));
+                        C.lhit(); nhits++;
+                    }
+                }
+            }
+        }
+        const int32_t left = n.left;
+        if (left >= 0) {
+            double lt, rt2;
+            C.aabb(2);
+            bool lh = aabb_hit(load3(n.lmin), load3(n.lmax), o, d, lt);
+            bool rh = aabb_hit(load3(n.rmin), load3(n.rmax), o, d, rt2);
+            if (lh) {
+                if (rh) S.push((uint32_t)n.right, 0.0);
+                node = (uint32_t)left;
+                continue;
+            }
+            if (rh) { node = (uint32_t)n.right; continue; }
+        }
+        if (S.sp == 0) break;
+        double tt;
+        S.pop(node, tt);
+    }
+}
+
+// intersect_lights (intersections.rs:87-91): boxes, ellipsoids, triangles
+template <bool ST>
+RT_D double lights_impact(const DevScene& S, V3 o, V3 d, Stack& stk, Cnt<ST>& C, uint32_t& nhits) {
+    double impact = 0.0;
+    bvh_all<1, ST>(S.lboxes, o, d, stk, C, impact, nhits);
+    bvh_all<2, ST>(S.lells, o, d, stk, C, impact, nhits);
+    bvh_all<3, ST>(S.ltris, o, d, stk, C, impact, nhits);
+    return impact;
+}
+template <bool ST>
+RT_D double light_pdf(const DevScene& S, V3 pos, V3 dir, Stack& stk, Cnt<ST>& C) {  // ray_sampler.rs:132-139
+    C.lq();
+    uint32_t nh = 0;
+    double impact = lights_impact<ST>(S, pos + dir * kEpsilon, dir, stk, C, nh);
+    return impact / (double)S.n_lights;
+}
+
+// ------------------------------------------------------------ samplers ----
+RT_D V3 uniform_on_sphere(Rng& r) {  // ray_sampler.rs:159-170
+    double a0 = gen_f64(r), a1 = gen_f64(r), a2 = gen_f64(r);
+    return normalize(v3(a0 * 2.0 - 1.0, a1 * 2.0 - 1.0, a2 * 2.0 - 1.0));
+}
+RT_D V3 cosine_sample(V3 n, Rng& r) {  // ray_sampler.rs:69-76
+    V3 v = uniform_on_sphere(r);
+    V3 d = v + n;
+    const double eps = kEpsilon * 16.0;
+    if (fabs(d.x) <= eps && fabs(d.y) <= eps && fabs(d.z) <= eps) return n;
+    return normalize(d);
+}
+RT_D double cosine_pdf(V3 n, V3 d) {  // ray_sampler.rs:78-83
+    if (dot(n, d) <= 0.0) return 0.0;
+    return dot(n, d) / kPi;
+}
+struct Scales { double s01, s11; };  // new_inclusive scales for [0,1] and [-1,1]
+RT_D V3 uniform_on_box(V3 s, Rng& r, const Scales& sc) {  // ray_sampler.rs:142-157
+    double w4x = s.y * s.z, w4y = s.x * s.z, w4z = s.x * s.y;
+    double choice = gen_range(r, 0.0, (w4x + w4y) + w4z);
+    double sign = (double)(gen_sign_bit(r) * 2 - 1);
+    double u1 = gen_range_incl(r, -1.0, sc.s11);
+    double u2 = gen_range_incl(r, -1.0, sc.s11);
+    V3 p;
+    if (choice < w4x) p = v3(sign, u1, u2);
+    else if (choice < w4x + w4y) p = v3(u1, sign, u2);
+    else p = v3(u1, u2, sign);
+    return mul(p, s);
+}
+RT_D V3 light_sample(const DevScene& S, V3 pos, Rng& r, const Scales& sc) {  // ray_sampler.rs:101-130
+    uint64_t index = gen_index(r, S.n_lights);
+    const uint32_t nb = S.lboxes.n_prims, ne = S.lells.n_prims;
+    V3 world;
+    if (index < nb) {
+        const DevShape l = S.lboxes.shapes[index];
+        world = rotate(load_quat(l.rot), uniform_on_box(load3(l.shape), r, sc)) + load3(l.pos);
+    } else if (index < (uint64_t)nb + ne) {
+        const DevShape l = S.lells.shapes[index - nb];
+        world = rotate(load_quat(l.rot), mul(uniform_on_sphere(r), load3(l.shape))) + load3(l.pos);
+    } else {
+        const DevTri t = S.ltris.tris[index - nb - ne];
+        double u = gen_range_incl(r, 0.0, sc.s01);
+        double v = gen_range_incl(r, 0.0, sc.s01);
+        if (u + v > 1.0) { u = 1.0 - u; v = 1.0 - v; }
+        world = (load3(t.ba) * u + load3(t.ca) * v) + load3(t.a);
+    }
+    return normalize(world - pos);
+}
+
+// --------------------------------------------------------- integrator ----
+RT_D double powi5(double x) { double x2 = x * x; return x * (x2 * x2); }
+
+struct PathState {
+    V3 o, d;       // current ray
+    V3 T;          // throughput
+    V3 L;          // radiance of this path so far
+};
+
+// One segment of raytrace_impl (raytrace.rs:12-60) in throughput form.
+// Returns true when the path continues with the updated ray.
+template <bool ST>
+RT_D bool segment(const DevScene& S, const KParams& P, const Scales& sc, PathState& ps, Rng& rng,
+                  Stack& stk, Cnt<ST>& C, int32_t& hit_gid) {
+    Hit h; uint32_t mat; int32_t gid;
+    C.segment();
+    if (!scene_intersect<ST>(S, ps.o, ps.d, stk, C, h, mat, gid)) {
+        hit_gid = RT_HIT_MISS;
+        ps.L = ps.L + mul(ps.T, load3(P.bg));
+        return false;
+    }
+    hit_gid = gid;
+    const DevMaterial& m = S.mats[mat];
+    const V3 col = load3(m.color);
+    ps.L = ps.L + mul(ps.T, load3(m.emission));
+    const V3 o = ps.o, d = ps.d;
+    if (m.kind == RT_MAT_DIFFUSE) {  // :16-34
+        V3 pos = o + d * h.t;
+        const bool empty = S.n_lights == 0;
+        V3 dir;
+        if (empty || gen_bool(rng, 0.5)) dir = cosine_sample(h.ns, rng);   // Mix::sample (ray_sampler.rs:87-93)
+        else dir = light_sample(S, pos, rng, sc);
+        const double cs = dot(dir, h.ns);
+        if (cs <= 0.0) return false;
+        double pdf = empty ? cosine_pdf(h.ns, dir)
+                           : (cosine_pdf(h.ns, dir) + light_pdf<ST>(S, pos, dir, stk, C)) / 2.0;  // Mix::pdf
+        if (pdf == 0.0) return false;
+        V3 w = v3(((cs * col.x) / kPi) / pdf, ((cs * col.y) / kPi) / pdf, ((cs * col.z) / kPi) / pdf);
+        ps.T = mul(ps.T, w);
+        ps.o = pos + dir * kEpsilon;
+        ps.d = dir;
+        return true;
+    }
+    // reflected_ray (raytrace.rs:67-73)
+    const V3 rdir = d - (h.ns * 2.0) * dot(h.ns, d);
+    const V3 hp = o + d * h.t;
+    if (m.kind == RT_MAT_DIELECTRIC) {  // :36-54
+        double n1 = 1.0, n2 = m.ior;
+        if (h.inside) { double t = n1; n1 = n2; n2 = t; }
+        const double k = n1 / n2;
+        // refracted_ray (raytrace.rs:75-88)
+        const double cos1 = -dot(h.ns, d);
+        const double sin2 = k * sqrt(1.0 - cos1 * cos1);
+        bool reflect = true;
+        if (!(sin2 > 1.0)) {
+            const double r0 = ((n1 - n2) / (n1 + n2)) * ((n1 - n2) / (n1 + n2));  // powi(_, 2)
+            const double power = r0 + (1.0 - r0) * powi5(1.0 + dot(d, h.ns));   // reflection_power
+            double p = power;
+            if (p < 0.0) p = 0.0;
+            if (p > 1.0) p = 1.0;
+            reflect = gen_bool(rng, p);
+            if (!reflect) {
+                const double cos2 = sqrt(1.0 - sin2 * sin2);
+                const V3 tdir = d * k + h.ns * (k * cos1 - cos2);
+                ps.o = hp + tdir * kEpsilon;
+                ps.d = tdir;
+                if (!h.inside) ps.T = mul(ps.T, col);
+            }
+        }
+        if (reflect) { ps.o = hp + rdir * kEpsilon; ps.d = rdir; }
+        return true;
+    }
+    // Metallic (:56-58)
+    ps.o = hp + rdir * kEpsilon;
+    ps.d = rdir;
+    ps.T = mul(ps.T, col);
+    return true;
+}
+
+template <bool ST>
+RT_D void wave_flush(const Cnt<ST>& C, unsigned long long* stats) {
+    if (!ST) return;
+    uint32_t v[8] = {C.c.paths, C.c.segments, C.c.aabb, C.c.tri, C.c.shape, C.c.shaded, C.c.lq, C.c.lhits};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        unsigned long long x = v[k];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+        if ((threadIdx.x & 63) == 0 && x) atomicAdd(&stats[k], x);
+    }
+}
+
+// ------------------------------------------------------------ kernels ----
+template <bool ST, bool HIT>
+__global__ __launch_bounds__(kBlock) void path_kernel(DevScene S, KParams P, double* __restrict__ out,
+                                                      int32_t* __restrict__ hit_ids,
+                                                      unsigned long long* __restrict__ stats,
+                                                      uint32_t* spill_n, double* spill_t) {
+    __shared__ uint32_t s_n[kShort * kBlock];
+    __shared__ double s_t[kShort * kBlock];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t slot = blockIdx.x;
+    const uint64_t tile = (uint64_t)P.rank + slot * P.world;
+    const uint32_t wave = tid >> 6, lane = tid & 63;
+    const uint32_t lx = (wave & 1u) * 8u + (lane & 7u), ly = (wave >> 1) * 8u + (lane >> 3);
+    double* o = out + (slot * (uint64_t)kBlock + ly * RT_TILE + lx) * 3;
+    Cnt<ST> C;
+    C.zero();
+    V3 sum = v3(0.0, 0.0, 0.0);
+    const uint32_t px = (uint32_t)(tile % P.tiles_x) * RT_TILE + lx;
+    const uint32_t py = (uint32_t)(tile / P.tiles_x) * RT_TILE + ly;
+    if (tile < P.n_tiles && px < P.width && py < P.height) {
+        Stack stk;
+        stk.sn = s_n + tid; stk.st = s_t + tid;
+        const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
+        stk.gn = spill_n ? spill_n + gtid : nullptr;
+        stk.gt = spill_t ? spill_t + gtid : nullptr;
+        stk.stride = (uint32_t)gridDim.x * kBlock;
+        stk.sp = 0;
+        const Scales sc{P.scale01, P.scale11};
+        const uint64_t pixel = (uint64_t)py * P.width + px;
+        const uint32_t spp = P.spp, depth = P.ray_depth;
+        PathState ps;
+        Rng rng;
+        uint32_t s = 0, b = 0;
+        bool fresh = true;
+        for (;;) {
+            if (fresh) {  // Camera::fuzzy_ray + raytrace (camera.rs:48-55, raytrace.rs:8-10)
+                if (s >= spp) break;
+                rng_init(rng, P.seed, pixel, s);
+                const double fx = (double)px + gen_range(rng, 0.0, 1.0);
+                const double fy = (double)py + gen_range(rng, 0.0, 1.0);
+                const double x = (2.0 * fx / P.fw - 1.0) * P.tan_x;
+                const double y = -(2.0 * fy / P.fh - 1.0) * P.tan_y;
+                const V3 dir = (load3(P.cam_right) * x + load3(P.cam_up) * y) + load3(P.cam_fwd) * 1.0;
+                ps.o = load3(P.cam_pos);
+                ps.d = normalize(dir);
+                ps.T = v3(1.0, 1.0, 1.0);
+                ps.L = v3(0.0, 0.0, 0.0);
+                b = 0;
+                fresh = false;
+                C.path();
+            }
+            bool cont = false;
+            if (b < depth) {
+                int32_t g;
+                cont = segment<ST>(S, P, sc, ps, rng, stk, C, g);
+                if (HIT) hit_ids[(pixel * spp + s) * depth + b] = g;
+                ++b;
+            }
+            if (!cont || b >= depth) {
+                if (HIT) for (uint32_t k = b; k < depth; ++k) hit_ids[(pixel * spp + s) * depth + k] = RT_HIT_NONE;
+                sum = sum + ps.L;
+                ++s;
+                fresh = true;
+            }
+        }
+        sum = sum / (double)spp;  // main.rs:104 (mean, before tonemapping)
+    }
+    o[0] = sum.x; o[1] = sum.y; o[2] = sum.z;
+    wave_flush<ST>(C, stats);
+}
+
+__global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S, const double* __restrict__ rays, uint32_t n,
+                                                           rt_hit* __restrict__ out, uint32_t* spill_n,
+                                                           double* spill_t) {
+    __shared__ uint32_t s_n[kShort * kBlock];
+    __shared__ double s_t[kShort * kBlock];
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    Stack stk;
+    stk.sn = s_n + threadIdx.x; stk.st = s_t + threadIdx.x;
+    stk.gn = spill_n ? spill_n + i : nullptr; stk.gt = spill_t ? spill_t + i : nullptr;
+    stk.stride = gridDim.x * kBlock; stk.sp = 0;
+    Cnt<false> C;
+    Hit h; uint32_t mat; int32_t gid;
+    V3 o = load3(rays + 6 * (size_t)i), d = load3(rays + 6 * (size_t)i + 3);
+    rt_hit r;
+    if (scene_intersect<false>(S, o, d, stk, C, h, mat, gid)) {
+        r.t = h.t; store3(r.geometry_normal, h.ng); store3(r.shading_normal, h.ns);
+        r.inside = h.inside ? 1 : 0; r.prim = gid;
+    } else {
+        r.t = 0.0; store3(r.geometry_normal, v3(0, 0, 0)); store3(r.shading_normal, v3(0, 0, 0));
+        r.inside = 0; r.prim = RT_HIT_MISS;
+    }
+    out[i] = r;
+}
+
+// mode 0: raw intersect_lights impact sum + hit count; mode 1: Light::pdf
+__global__ __launch_bounds__(kBlock) void light_kernel(DevScene S, const double* __restrict__ rays, uint32_t n,
+                                                       int mode, double* __restrict__ out, uint32_t* __restrict__ cnt,
+                                                       uint32_t* spill_n, double* spill_t) {
+    __shared__ uint32_t s_n[kShort * kBlock];
+    __shared__ double s_t[kShort * kBlock];
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    Stack stk;
+    stk.sn = s_n + threadIdx.x; stk.st = s_t + threadIdx.x;
+    stk.gn = spill_n ? spill_n + i : nullptr; stk.gt = spill_t ? spill_t + i : nullptr;
+    stk.stride = gridDim.x * kBlock; stk.sp = 0;
+    Cnt<false> C;
+    V3 o = load3(rays + 6 * (size_t)i), d = load3(rays + 6 * (size_t)i + 3);
+    uint32_t nh = 0;
+    double v;
+    if (mode == 0) v = lights_impact<false>(S, o, d, stk, C, nh);
+    else v = S.n_lights == 0 ? 0.0 : light_pdf<false>(S, o, d, stk, C);
+    out[i] = v;
+    if (cnt) cnt[i] = nh;
+}
+
+__global__ void unpack_kernel(const double* __restrict__ g, double* __restrict__ img, uint32_t W, uint32_t H,
+                              uint32_t tiles_x, uint32_t world, uint32_t per_rank) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (uint64_t)W * H) return;
+    const uint32_t x = (uint32_t)(i % W), y = (uint32_t)(i / W);
+    const uint64_t tile = (uint64_t)(y / RT_TILE) * tiles_x + x / RT_TILE;
+    const uint64_t rank = tile % world, slot = tile / world;
+    const double* src = g + (((rank * per_rank + slot) * kBlock) + (y % RT_TILE) * RT_TILE + (x % RT_TILE)) * 3;
+    img[3 * i] = src[0]; img[3 * i + 1] = src[1]; img[3 * i + 2] = src[2];
+}
+
+__global__ void fp64_probe_kernel(const double* a, const double* b, double* out, uint32_t n, int op) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = op == 0 ? sqrt(a[i]) : a[i] / b[i];
+}
+
+// ------------------------------------------------------------- launch ----
+hipError_t launch_path(const DevScene& S, const KParams& P, uint32_t n_slots, double* out, int32_t* hit_ids,
+                       unsigned long long* stats, uint32_t* spill_n, double* spill_t, hipStream_t st) {
+    dim3 grid(n_slots), block(kBlock);
+    const bool ST = stats != nullptr, HIT = hit_ids != nullptr;
+    if (ST && HIT) hipLaunchKernelGGL((path_kernel<true, true>), grid, block, 0, st, S, P, out, hit_ids, stats, spill_n, spill_t);
+    else if (ST) hipLaunchKernelGGL((path_kernel<true, false>), grid, block, 0, st, S, P, out, hit_ids, stats, spill_n, spill_t);
+    else if (HIT) hipLaunchKernelGGL((path_kernel<false, true>), grid, block, 0, st, S, P, out, hit_ids, stats, spill_n, spill_t);
+    else hipLaunchKernelGGL((path_kernel<false, false>), grid, block, 0, st, S, P, out, hit_ids, stats, spill_n, spill_t);
+    return hipGetLastError();
+}
+hipError_t launch_intersect(const DevScene& S, const double* rays, uint32_t n, rt_hit* out, uint32_t* spill_n,
+                            double* spill_t, hipStream_t st) {
+    uint32_t blocks = (n + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(intersect_kernel, dim3(blocks), dim3(kBlock), 0, st, S, rays, n, out, spill_n, spill_t);
+    return hipGetLastError();
+}
+hipError_t launch_light(const DevScene& S, const double* rays, uint32_t n, int mode, double* out, uint32_t* cnt,
+                        uint32_t* spill_n, double* spill_t, hipStream_t st) {
+    uint32_t blocks = (n + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(light_kernel, dim3(blocks), dim3(kBlock), 0, st, S, rays, n, mode, out, cnt, spill_n, spill_t);
+    return hipGetLastError();
+}
+hipError_t launch_unpack(const double* g, double* img, uint32_t W, uint32_t H, uint32_t tiles_x, uint32_t world,
+                         uint32_t per_rank, hipStream_t st) {
+    uint64_t n = (uint64_t)W * H;
+    hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, g, img, W, H, tiles_x,
+                       world, per_rank);
+    return hipGetLastError();
+}
+hipError_t launch_fp64_probe(const double* a, const double* b, double* out, uint32_t n, int op, hipStream_t st) {
+    hipLaunchKernelGGL(fp64_probe_kernel, dim3((n + 255) / 256), dim3(256), 0, st, a, b, out, n, op);
+    return hipGetLastError();
+}
+
+}  // namespace rt

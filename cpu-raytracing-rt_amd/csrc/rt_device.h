@@ -1,0 +1,258 @@
+// rt_device.h — device-side building blocks of the path tracer (gfx950).
+//
+// Everything here restates the reference's per-ray arithmetic in f64 with the
+// reference's operation order so that, on the same Philox stream, the device
+// produces bit-identical hit ids and radiance to the oracle's iterative form
+// (oracle/oracle.c raytrace_iter).  Cited reference lines are in
+// /root/reference/src.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "rt_layout.h"
+#include "rt_math.h"
+
+namespace rt {
+
+#define RT_D __device__ __forceinline__
+
+// ------------------------------------------------------------------ RNG ----
+// Counter-based Philox4x32-10 per (pixel, sample) replaces ThreadRng
+// (main.rs:95); ctr = {block, sample, pixel_lo, pixel_hi}, key = seed.
+// Words are consumed in order; next_u64 = lo word | hi word << 32 (rand
+// BlockRng order).  The 4-word block lives in two u64 "queues" so no
+// dynamically indexed register array (which would go to scratch).
+struct Rng {
+    uint32_t sample, pix_lo, pix_hi, k0, k1;
+    uint32_t blk;       // next block counter
+    uint32_t avail;     // words left in q0/q1
+    uint64_t q0, q1;
+};
+
+RT_D void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
+                 uint64_t& q0, uint64_t& q1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+        uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    }
+    q0 = (uint64_t)c0 | ((uint64_t)c1 << 32);
+    q1 = (uint64_t)c2 | ((uint64_t)c3 << 32);
+}
+RT_D void rng_init(Rng& r, uint64_t seed, uint64_t pixel, uint32_t sample) {
+    r.sample = sample; r.pix_lo = (uint32_t)pixel; r.pix_hi = (uint32_t)(pixel >> 32);
+    r.k0 = (uint32_t)seed; r.k1 = (uint32_t)(seed >> 32);
+    r.blk = 0; r.avail = 0; r.q0 = 0; r.q1 = 0;
+}
+RT_D uint32_t next_u32(Rng& r) {
+    if (r.avail == 0) {
+        philox(r.blk, r.sample, r.pix_lo, r.pix_hi, r.k0, r.k1, r.q0, r.q1);
+        r.blk++;
+        r.avail = 4;
+    }
+    uint32_t w = (uint32_t)r.q0;
+    r.q0 = (r.q0 >> 32) | (r.q1 << 32);
+    r.q1 >>= 32;
+    r.avail--;
+    return w;
+}
+RT_D uint64_t next_u64(Rng& r) {
+    uint64_t lo = next_u32(r);
+    uint64_t hi = next_u32(r);
+    return lo | (hi << 32);
+}
+// rand 0.8.5 transforms (see oracle.c header for the full list)
+RT_D double gen_f64(Rng& r) { return (double)(next_u64(r) >> 11) * (1.0 / 9007199254740992.0); }
+RT_D double value0_1(Rng& r) {
+    return __longlong_as_double((long long)((next_u64(r) >> 12) | 0x3FF0000000000000ull)) - 1.0;
+}
+RT_D double gen_range(Rng& r, double low, double high) {  // UniformFloat::sample_single
+    double scale = high - low;
+    for (;;) {
+        double res = value0_1(r) * scale + low;
+        if (res < high) return res;
+    }
+}
+RT_HD double inclusive_scale(double low, double high) {  // UniformFloat::new_inclusive
+    const double max_rand = 1.0 - 2.220446049250313080847263336181640625e-16;  // (u64::MAX>>12 | 1.0) - 1
+    double scale = (high - low) / max_rand;
+    while (scale * max_rand + low > high) {
+        uint64_t b;
+        __builtin_memcpy(&b, &scale, 8);
+        b -= 1;
+        __builtin_memcpy(&scale, &b, 8);
+    }
+    return scale;
+}
+RT_D double gen_range_incl(Rng& r, double low, double scale) { return value0_1(r) * scale + low; }
+RT_D uint64_t gen_index(Rng& r, uint64_t range) {  // UniformInt<usize>::sample_single(0..range)
+    uint64_t zone = (range << __clzll(range)) - 1;
+    for (;;) {
+        uint64_t v = next_u64(r);
+        uint64_t lo = v * range, hi = __umul64hi(v, range);
+        if (lo <= zone) return hi;
+    }
+}
+RT_D int32_t gen_sign_bit(Rng& r) {  // UniformInt<i32>::sample_single_inclusive(0, 1)
+    for (;;) {
+        uint32_t v = next_u32(r);
+        uint32_t lo = v << 1, hi = v >> 31;
+        if (lo <= 0x7FFFFFFFu) return (int32_t)hi;
+    }
+}
+RT_D bool gen_bool(Rng& r, double p) {  // Bernoulli
+    if (p == 1.0) return true;  // ALWAYS_TRUE, no draw
+    uint64_t p_int = (p >= 0.0 && p < 1.0) ? (uint64_t)(p * 18446744073709551616.0) : 0ull;
+    return next_u64(r) < p_int;
+}
+
+// ------------------------------------------------------------- counters ---
+struct Counters {
+    uint32_t segments, aabb, tri, shape, shaded, lq, lhits, paths;
+};
+template <bool ON>
+struct Cnt {
+    Counters c;
+    RT_D void zero() { if (ON) { c = Counters{0, 0, 0, 0, 0, 0, 0, 0}; } }
+    RT_D void segment() { if (ON) c.segments++; }
+    RT_D void aabb(uint32_t n = 1) { if (ON) c.aabb += n; }
+    RT_D void tri() { if (ON) c.tri++; }
+    RT_D void shape() { if (ON) c.shape++; }
+    RT_D void shaded() { if (ON) c.shaded++; }
+    RT_D void lq() { if (ON) c.lq++; }
+    RT_D void lhit() { if (ON) c.lhits++; }
+    RT_D void path() { if (ON) c.paths++; }
+};
+
+// ------------------------------------------------------------ geometry ----
+// AABB::intersects (aabb.rs:51-108)
+RT_D double safe_min(double a, double b) {
+    if (!isfinite(a)) return b;
+    if (!isfinite(b)) return a;
+    return rmin(a, b);
+}
+RT_D double safe_max(double a, double b) {
+    if (!isfinite(a)) return b;
+    if (!isfinite(b)) return a;
+    return rmax(a, b);
+}
+RT_D bool aabb_hit(V3 mn, V3 mx, V3 o, V3 d, double& t) {
+    if ((d.x == 0.0 && (o.x < mn.x || mx.x < o.x)) || (d.y == 0.0 && (o.y < mn.y || mx.y < o.y)) ||
+        (d.z == 0.0 && (o.z < mn.z || mx.z < o.z)))
+        return false;
+    if (!(o.x < mn.x || mx.x < o.x || o.y < mn.y || mx.y < o.y || o.z < mn.z || mx.z < o.z)) {
+        t = 0.0;  // inside (aabb.rs:58-60)
+        return true;
+    }
+    V3 tmin = div(mn - o, d), tmax = div(mx - o, d);
+    double t1x = safe_min(tmin.x, tmax.x), t1y = safe_min(tmin.y, tmax.y), t1z = safe_min(tmin.z, tmax.z);
+    double t2x = safe_max(tmin.x, tmax.x), t2y = safe_max(tmin.y, tmax.y), t2z = safe_max(tmin.z, tmax.z);
+    double tn = safe_max(safe_max(t1x, t1y), t1z);
+    double tf = safe_min(safe_min(t2x, t2y), t2z);
+    if (tn > tf) return false;
+    if (0.0 <= tn) { t = tn; return true; }
+    if (0.0 <= tf) { t = tf; return true; }
+    return false;
+}
+
+// model_space_ray (intersections.rs:93-99)
+RT_D void model_ray(const DevShape& s, V3 o, V3 d, V3& mo, V3& md) {
+    Quat r = conjugate(load_quat(s.rot));
+    mo = rotate(r, o - load3(s.pos));
+    md = rotate(r, d);
+}
+
+// Plane::intersection (plane.rs:11-21); aux bit0 = (nd <= 0)
+RT_D bool plane_t(V3 n, V3 o, V3 d, double& t, uint32_t& aux) {
+    double nd = dot(n, d);
+    double tt = -dot(n, o) / nd;
+    if (tt < 0.0) return false;
+    t = tt;
+    aux = nd <= 0.0 ? 1u : 0u;
+    return true;
+}
+
+// intersect_box_coef (box.rs:75-115). Entry/exit as (t, sign, dim).
+struct Bpi { double t; double sign; int dim; };
+RT_D int box_coef(V3 s, V3 o, V3 d, Bpi& en, Bpi& ex) {
+    bool have = false;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        double di = comp(d, i), oi = comp(o, i), si = comp(s, i);
+        if (di == 0.0 && si < fabs(oi)) return 0;
+        if (di == 0.0) continue;
+        double t1 = (si - oi) / di, t2 = (-si - oi) / di;
+        double a, b, nrm;
+        if (t1 < t2) { a = t1; b = t2; nrm = 1.0; } else { a = t2; b = t1; nrm = -1.0; }
+        if (!have) { en = Bpi{a, nrm, i}; ex = Bpi{b, nrm, i}; have = true; }
+        else {
+            if (!(a < en.t)) en = Bpi{a, nrm, i};   // BoxPlaneIntersection::max (box.rs:57-59)
+            if (b < ex.t) ex = Bpi{b, nrm, i};      // BoxPlaneIntersection::min (box.rs:60-62)
+        }
+    }
+    if (!have) return 0;
+    if (ex.t < en.t) return 0;
+    if (0.0 <= en.t) return 2;
+    if (0.0 <= ex.t) return 1;
+    return 0;
+}
+RT_D V3 bpi_normal(const Bpi& p) {  // box.rs:64-72
+    if (p.dim == 0) return v3(p.sign, 0.0, 0.0);
+    if (p.dim == 1) return v3(0.0, p.sign, 0.0);
+    return v3(0.0, 0.0, p.sign);
+}
+// aux encodes the returned face: bits0-1 dim, bit2 sign(+1), bit3 inside
+RT_D uint32_t bpi_aux(const Bpi& p, bool inside) {
+    return (uint32_t)p.dim | (p.sign > 0.0 ? 4u : 0u) | (inside ? 8u : 0u);
+}
+RT_D V3 aux_box_normal(uint32_t aux) {
+    double s = (aux & 4u) ? 1.0 : -1.0;
+    uint32_t dim = aux & 3u;
+    if (dim == 0) return v3(s, 0.0, 0.0);
+    if (dim == 1) return v3(0.0, s, 0.0);
+    return v3(0.0, 0.0, s);
+}
+
+// intersect_ellipsoid_coef (ellipsoid.rs:49-76)
+RT_D int ell_coef(V3 r, V3 o, V3 d, double& t1o, double& t2o) {
+    V3 oo = div(o, r), dd = div(d, r);
+    double c = dot(oo, oo), b = dot(oo, dd), a = dot(dd, dd);
+    double disc = b * b - a * (c - 1.0);
+    if (disc < 0.0) return 0;
+    double ds = sqrt(disc);
+    double t1 = (-b + ds) / a, t2 = (-b - ds) / a;
+    if (t2 < t1) { double tmp = t1; t1 = t2; t2 = tmp; }
+    t1o = t1; t2o = t2;
+    if (0.0 <= t1) return 2;
+    if (0.0 <= t2) return 1;
+    return 0;
+}
+RT_D V3 ell_normal(V3 r, V3 o, V3 d, double t) {  // ellipsoid.rs:26,29
+    V3 p = o + d * t;
+    return normalize(div(div(p, r), r));
+}
+
+// Triangle::intersection (triangle.rs:49-80) up to (u, v, t); normals later.
+RT_D bool tri_uvt(const DevTri& tr, V3 o, V3 d, double& u, double& v, double& t) {
+    V3 m0 = load3(tr.ba), m1 = load3(tr.ca), m2 = -d;
+    double det = m0.x * (m1.y * m2.z - m2.y * m1.z) - m1.x * (m0.y * m2.z - m2.y * m0.z) +
+                 m2.x * (m0.y * m1.z - m1.y * m0.z);
+    if (fabs(det) < 1e-11) return false;
+    V3 x0 = cross(m1, m2) / det, x1 = cross(m2, m0) / det, x2 = cross(m0, m1) / det;
+    V3 w = o - load3(tr.a);
+    double uu = dot(x0, w), vv = dot(x1, w), tt = dot(x2, w);
+    if (uu < 0.0 || vv < 0.0 || 1.0 < uu + vv || tt < 0.0) return false;
+    u = uu; v = vv; t = tt;
+    return true;
+}
+
+// Intersection (intersections.rs:10-16)
+struct Hit { double t; V3 ng, ns; bool inside; };
+
+RT_D Hit rotated(const Hit& h, Quat q) {  // with_rotated_normal (intersections.rs:32-39)
+    return Hit{h.t, normalize(rotate(q, h.ng)), normalize(rotate(q, h.ns)), h.inside};
+}
+
+}  // namespace rt

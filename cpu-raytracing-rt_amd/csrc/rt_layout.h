@@ -1,0 +1,78 @@
+// rt_layout.h — the scene as it lives in HBM.
+//
+// The reference's scene (scene.rs:56-90) is a tree of Rust structs; here it is
+// flattened into read-only arrays split into HOT data (read on every test) and
+// COLD data (read once per shaded hit):
+//   * BVH nodes: pre-order like bvh.rs:104 (root = 0, left child = node + 1),
+//     one 128-B "fat" node per node holding BOTH children's f64 boxes, so a
+//     visit is one aligned 128-B line (the reference reads two 80-B Nodes
+//     scattered in a Vec, bvh.rs:158-159).
+//   * shapes (plane/box/ellipsoid): 80-B hot record {shape, position, rotation}
+//     = the model-space transform of intersections.rs:93-99.
+//   * triangles: 80-B hot record {a, ba, ca} (the 3x3 solve of
+//     triangle.rs:49-67); normals / 1/area / material in cold SoA arrays.
+#pragma once
+#include <stdint.h>
+
+namespace rt {
+
+constexpr int kMaxBvhDepthShort = 12;   // per-lane short stack kept in LDS
+
+struct alignas(128) DevNode {
+    double lmin[3], lmax[3];   // left child's box  (bvh.rs:158)
+    double rmin[3], rmax[3];   // right child's box (bvh.rs:159)
+    int32_t left, right;       // child indices, -1 for a leaf
+    uint32_t start, count;     // leaf primitive range [start, start+count)
+};
+static_assert(sizeof(DevNode) == 128, "fat node is one 128-B line");
+
+struct alignas(16) DevShape {  // Primitive<T> hot part (scene.rs:20-27)
+    double shape[3];           // plane normal | box half sizes | ellipsoid radii
+    double pos[3];
+    double rot[4];             // (s, x, y, z)
+};
+static_assert(sizeof(DevShape) == 80, "shape record");
+
+struct alignas(16) DevTri {    // Triangle hot part (triangle.rs:5-17)
+    double a[3], ba[3], ca[3];
+    double pad;
+};
+static_assert(sizeof(DevTri) == 80, "triangle record");
+
+struct DevTriCold {            // read only on a hit
+    double ng[3], na[3], nb[3], nc[3];
+};
+
+struct DevMaterial {           // Metadata (scene.rs:13-18)
+    uint32_t kind, pad;
+    double ior;
+    double color[3], emission[3];
+};
+
+struct DevBvh {
+    const DevNode* nodes;
+    double root_min[3], root_max[3];
+    uint32_t n_prims;
+    uint32_t depth;            // levels (root = 1)
+    // primitives in BVH order: exactly one of these is non-null
+    const DevShape* shapes;
+    const DevTri* tris;
+    const DevTriCold* tri_cold;
+    const double* tri_inv_area;
+    const uint32_t* mat;       // material per primitive
+    const int32_t* gid;        // global primitive id per primitive
+};
+
+struct DevScene {
+    uint32_t n_planes;
+    uint32_t n_lights;         // boxes + ellipsoids + triangles in the light BVHs
+    const DevShape* planes;
+    const uint32_t* plane_mat;
+    const int32_t* plane_gid;
+    DevBvh boxes, ells, tris;          // ScenePrimitives (scene.rs:56-62)
+    DevBvh lboxes, lells, ltris;       // LightPrimitives (scene.rs:64-69)
+    const DevMaterial* mats;
+    uint32_t max_depth;                // max BVH depth over the six (stack bound)
+};
+
+}  // namespace rt

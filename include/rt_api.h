@@ -1,0 +1,241 @@
+/*
+ * rt_api.h — C ABI of the MI355X-native path-tracing hot path.
+ *
+ * Drop-in boundary for uncerso/cpu-raytracing-rt (Rust, CPU).  The reference
+ * has no FFI: its only seam is `generate_image(&Scene) -> Image`
+ * (src/main.rs:85-114), called once per frame by `main` (src/main.rs:73).
+ * Every entry point below names the reference item it replaces.  All
+ * signatures are plain C (PODs, pointers, sizes) so a Rust host can bind them
+ * with `extern "C"` + `#[repr(C)]`, or Python via ctypes.
+ *
+ * Conventions
+ *  - Return value: 0 (RT_OK) on success, a negative rt_error otherwise.  Nothing
+ *    unwinds or aborts across the ABI (the reference panics instead:
+ *    src/gltf/scene_builder.rs:58,210,212, src/scene.rs:188).  The message of the
+ *    last failure on the calling thread is available from rt_last_error().
+ *  - Ownership: the caller owns every host buffer; arrays in descriptors are
+ *    BORROWED for the duration of the call.  The library owns device memory
+ *    behind opaque handles.
+ *  - Numerics: f64 everywhere, like the reference (src/types.rs:5).
+ *  - Threading: one host thread per handle (a handle is not re-entrant), as
+ *    the reference calls its pixel loop once from the main thread.
+ */
+#ifndef RT_API_H
+#define RT_API_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_API_VERSION 1
+
+typedef enum rt_error {
+    RT_OK = 0,
+    RT_ERR_INVALID = -1,     /* bad argument / inconsistent descriptor            */
+    RT_ERR_DEVICE = -2,      /* HIP runtime error (no device, launch failure ...) */
+    RT_ERR_NOMEM = -3,       /* host or device allocation failed                  */
+    RT_ERR_PARSE = -4,       /* scene text / glTF JSON could not be parsed        */
+    RT_ERR_IO = -5,          /* file could not be read or written                 */
+    RT_ERR_UNSUPPORTED = -6  /* input the reference also rejects (e.g. glTF mode!=4) */
+} rt_error;
+
+/* ---- materials: src/scene.rs:6-18 (Material, Metadata) ------------------- */
+enum { RT_MAT_DIFFUSE = 0, RT_MAT_METALLIC = 1, RT_MAT_DIELECTRIC = 2 };
+
+typedef struct rt_material {
+    uint32_t kind;        /* RT_MAT_*                                         */
+    uint32_t _pad;
+    double ior;           /* Material::Dielectric(ior); ignored otherwise      */
+    double color[3];      /* Metadata::color    (default 0, scene.rs:102)      */
+    double emission[3];   /* Metadata::emission (!= 0 => light, scene.rs:225)  */
+} rt_material;
+
+/* ---- analytic shapes: src/primitives/{plane,box,ellipsoid}.rs ------------ */
+enum { RT_SHAPE_PLANE = 0, RT_SHAPE_BOX = 1, RT_SHAPE_ELLIPSOID = 2 };
+
+typedef struct rt_shape {
+    uint32_t type;        /* RT_SHAPE_*                                        */
+    uint32_t material;    /* index into rt_scene_desc.materials                */
+    double shape[3];      /* plane normal | box half-sizes | ellipsoid radii   */
+    double position[3];   /* Primitive::position (default 0, scene.rs:110)     */
+    double rotation[4];   /* Primitive::rotation as (s, x, y, z); NOT normalised,
+                             exactly as parsed (scene_parser.rs:51-57)         */
+} rt_shape;
+
+/* ---- triangles ------------------------------------------------------------ */
+enum {
+    /* custom-format TRIANGLE: Triangle::new_with_geometry_normals then
+       TrianglePrimitive::new (rotate+translate, props recomputed)
+       (scene_parser.rs:71-73, scene.rs:139-165)                                */
+    RT_TRI_CUSTOM = 0,
+    /* glTF: world-space vertices+normals, Triangle::new_with_smooth_normal then
+       `instantiate` (AABB of a, a+ba, a+ca) (gltf/scene_builder.rs:42-55,329-356) */
+    RT_TRI_GLTF = 1
+};
+
+/*
+ * Scene description = the reference's parsed scene (parsed_scene.rs:4-75 for
+ * the custom format; the flattened triangle list of gltf/scene_builder.rs for
+ * glTF).  Shapes and triangles are each in INPUT order; the library splits them
+ * per kind preserving relative order and builds the six BVHs exactly as
+ * make_scenes does (scene.rs:194-223).  Global primitive id (used by hit-id
+ * dumps): shape i -> i, triangle j -> n_shapes + j.
+ */
+typedef struct rt_scene_desc {
+    uint32_t n_materials;
+    uint32_t n_shapes;
+    uint64_t n_triangles;
+    const rt_material* materials;
+    const rt_shape* shapes;
+    uint32_t tri_mode;              /* RT_TRI_CUSTOM | RT_TRI_GLTF            */
+    uint32_t _pad;
+    const double* tri_vertices;     /* [n][3][3]: a, b, c                     */
+    const double* tri_normals;      /* [n][3][3]: na, nb, nc (GLTF only)      */
+    const double* tri_position;     /* [n][3] (CUSTOM only; NULL => 0)        */
+    const double* tri_rotation;     /* [n][4] (s,x,y,z) (CUSTOM; NULL => id)  */
+    const uint32_t* tri_material;   /* [n]                                    */
+} rt_scene_desc;
+
+/* ---- camera: src/scene.rs:36-49 (Fov, CameraParams), src/camera.rs ------- */
+enum { RT_FOV_X = 0, RT_FOV_Y = 1 };
+
+/* flags */
+#define RT_FLAG_STATS        0x1u  /* fill rt_stats work counters (separate untimed pass) */
+#define RT_FLAG_HIT_IDS      0x2u  /* dump (pixel, sample, bounce) -> global primitive id */
+
+typedef struct rt_render_params {
+    uint32_t width, height;        /* Scene::dimensions                        */
+    uint32_t spp;                  /* Scene::samples                           */
+    uint32_t ray_depth;            /* Scene::ray_depth (u8 in the reference)   */
+    double bg_color[3];            /* Scene::bg_color                          */
+    double cam_position[3];        /* CameraParams (already normalised for the
+                                      custom format, scene.rs:169-175)         */
+    double cam_right[3], cam_up[3], cam_forward[3];
+    uint32_t fov_axis;             /* RT_FOV_X | RT_FOV_Y                      */
+    uint32_t flags;                /* RT_FLAG_*                                */
+    double fov;                    /* radians                                  */
+    uint64_t seed;                 /* counter-based RNG key (replaces the
+                                      OS-seeded thread_rng, main.rs:95)        */
+} rt_render_params;
+
+/* Work counters of one render (canonical byte model: DESIGN.md §4). */
+typedef struct rt_stats {
+    uint64_t paths;            /* camera paths = W*H*spp                         */
+    uint64_t segments;         /* closest-hit queries (raytrace.rs:14) = samples */
+    uint64_t aabb_tests;       /* AABB::intersects calls (aabb.rs:51)            */
+    uint64_t tri_tests;        /* Triangle::intersection calls                   */
+    uint64_t shape_tests;      /* plane/box/ellipsoid intersection calls         */
+    uint64_t shaded_hits;      /* closest hits returned to the integrator        */
+    uint64_t light_queries;    /* Light::pdf all-hits queries                    */
+    uint64_t light_hits;       /* callbacks of intersect_lights                  */
+    double   kernel_ms;        /* device time of the path kernel(s)              */
+    double   total_ms;         /* wall time of rt_render incl. copies            */
+} rt_stats;
+
+/* Hit-id sentinels in the (pixel, sample, bounce) dump */
+#define RT_HIT_MISS      (-1)   /* closest-hit query returned None -> bg_color   */
+#define RT_HIT_NONE      (-2)   /* bounce not reached (path ended earlier)       */
+
+/* Ray-query result (intersections.rs:10-16 Intersection + winner id). */
+typedef struct rt_hit {
+    double t;
+    double geometry_normal[3];  /* world space, rotated+normalised (intersections.rs:32-39) */
+    double shading_normal[3];
+    int32_t inside;
+    int32_t prim;               /* global primitive id or RT_HIT_MISS            */
+} rt_hit;
+
+typedef struct rt_scene rt_scene;            /* opaque, device-resident       */
+typedef struct rt_parsed_scene rt_parsed_scene; /* opaque, host-side parse result */
+
+/* ======================= scene lifetime =================================== */
+/* Replaces Scene::new + make_scenes (src/scene.rs:180-223) and BVH::new
+   (src/bvh.rs:12-17); uploads the flattened scene to the CURRENT HIP device. */
+int  rt_scene_create(const rt_scene_desc* desc, rt_scene** out);
+void rt_scene_destroy(rt_scene* scene);
+
+typedef struct rt_scene_info {
+    uint32_t n_planes, n_boxes, n_ellipsoids;
+    uint64_t n_triangles;
+    uint32_t n_light_boxes, n_light_ellipsoids;
+    uint64_t n_light_triangles;
+    uint64_t bvh_nodes[6];       /* boxes, ellipsoids, triangles, light boxes, light ellipsoids, light triangles */
+    uint32_t bvh_depth[6];
+    double   build_ms;           /* host BVH build                                */
+    double   upload_ms;          /* H2D copy                                      */
+    uint64_t device_bytes;
+} rt_scene_info;
+int rt_scene_get_info(const rt_scene* scene, rt_scene_info* out);
+
+/* ======================= the frame (hot path) ============================= */
+/* Replaces generate_image's pixel loop (src/main.rs:85-103): for every pixel,
+   the mean over spp of raytrace(Camera::fuzzy_ray(px)) (camera.rs:48-55,
+   raytrace.rs:8-60).  out_mean_rgb: caller-owned [H][W][3] f64, row-major
+   idx = y*W + x (main.rs:96-97), BEFORE aces_tonemap/correct_gamma
+   (main.rs:104).  opt_hit_ids: NULL or caller-owned [W*H][spp][ray_depth]
+   int32 (requires RT_FLAG_HIT_IDS).  opt_stats: NULL or filled. */
+int rt_render(rt_scene* scene, const rt_render_params* params,
+              double* out_mean_rgb, int32_t* opt_hit_ids, rt_stats* opt_stats);
+
+/* Multi-GPU tile partition: 16x16 tiles, tile t belongs to
+   rank t % world.  Each rank renders its tiles into a packed DEVICE buffer
+   [n_tiles_padded][256][3] f64 (n_tiles_padded = ceil(total_tiles/world)),
+   asynchronously on `hip_stream` (NULL = default stream). */
+#define RT_TILE 16
+int rt_tiles_per_rank(const rt_render_params* params, uint32_t world, uint32_t* n_tiles_padded);
+int rt_render_tiles_async(rt_scene* scene, const rt_render_params* params,
+                          uint32_t rank, uint32_t world,
+                          double* d_tile_rgb, void* hip_stream);
+/* Root side after the gather: d_gathered = [world][n_tiles_padded][256][3]
+   (rank-major, as ncclGather lays it out) -> d_image [H][W][3]. */
+int rt_unpack_tiles_async(const rt_render_params* params, uint32_t world,
+                          const double* d_gathered, double* d_image, void* hip_stream);
+
+/* ======================= ray queries ====================================== */
+/* Closest hit for a batch of world rays [n][6] = (origin, dir) — replaces
+   intersections.rs:42-62 `intersect(ray, &scene.primitives, +inf)`. */
+int rt_intersect_rays(rt_scene* scene, const double* rays, uint32_t n, rt_hit* out);
+/* Light-area pdf for a batch [n][6] = (surface pos, unit dir) — replaces
+   ray_sampler.rs:132-139 Light::pdf (all-hits query intersections.rs:87-91). */
+int rt_light_pdf_rays(rt_scene* scene, const double* pos_dir, uint32_t n, double* out_pdf);
+/* The raw intersect_lights accumulation of Light::pdf for rays [n][6] used as
+   given (no EPSILON offset, no 1/len): out_impact = sum over every light
+   crossing of p_area * t^2/|d.n_g|; out_count = number of callbacks
+   (intersections.rs:87-91; known-answer test primitives/triangle.rs:98-128). */
+int rt_intersect_lights_rays(rt_scene* scene, const double* rays, uint32_t n,
+                             double* out_impact, uint32_t* out_count);
+
+/* ======================= host input surface =============================== */
+/* Custom text format (src/scene_parser.rs:5-85, defaults scene.rs:167-191). */
+int rt_parse_custom_scene(const char* text, rt_parsed_scene** out);
+/* glTF subset (src/gltf/parser.rs, src/gltf/scene_builder.rs:9-22); external
+   .bin buffers resolved relative to the .gltf path (main.rs:54-59,77-83). */
+int rt_load_gltf(const char* gltf_path, uint32_t width, uint32_t height,
+                 uint32_t spp, rt_parsed_scene** out);
+/* Views into the parse result (valid until rt_parsed_scene_free). */
+int rt_parsed_scene_get(const rt_parsed_scene* ps, rt_scene_desc* desc,
+                        rt_render_params* params);
+void rt_parsed_scene_free(rt_parsed_scene* ps);
+
+/* ======================= host output surface ============================== */
+/* correct_gamma(aces_tonemap(x)) per pixel (postprocessing.rs:5-37). */
+void rt_tonemap_gamma(const double* mean_rgb, uint64_t n_pixels, double* out_rgb);
+/* Binary P6 PPM of an already tonemapped image (ppm.rs:4-19). */
+int rt_save_ppm(const char* path, uint32_t width, uint32_t height, const double* rgb);
+
+/* ======================= misc ============================================= */
+const char* rt_last_error(void);
+int rt_api_version(void);
+/* Number of visible HIP devices (0 when none); never fails. */
+int rt_device_count(void);
+/* Diagnostic: device f64 sqrt (op 0) or a/b (op 1) for n values, to check that
+   the device rounds like the host (the bit-exact parity premise). */
+int rt_probe_fp64(int op, const double* a, const double* b, uint32_t n, double* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_API_H */

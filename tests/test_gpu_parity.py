@@ -1,0 +1,164 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle.
+
+Bar:
+  * hit ids (pixel, sample, bounce) -> global primitive id: bit-exact vs the
+    oracle (both the device-form and the recursive form of raytrace_impl);
+  * mean radiance: bit-exact vs the oracle's iterative form (the device
+    algorithm), and within REL_TOL per channel of the recursive restatement of
+    raytrace_impl (raytrace.rs:12-60), whose summation order differs;
+  * work counters (segments, AABB/triangle/shape tests, light queries) equal.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+# recursive (e + f*(e + f*(...))) vs throughput (sum T*e) association: f64
+# rounding only, a handful of ulps per bounce.
+REL_TOL = 1e-12
+
+
+@pytest.fixture(scope="module")
+def cornell(rt, orc, scene_text):
+    desc, params = rt.parse_scene(scene_text("cornell.txt"))
+    return desc, params, rt.Scene(desc), orc.OracleScene(desc)
+
+
+@pytest.fixture(scope="module")
+def sink(rt, orc, scene_text):
+    desc, params = rt.parse_scene(scene_text("kitchen_sink.txt"))
+    return desc, params, rt.Scene(desc), orc.OracleScene(desc)
+
+
+def _compare(gpu_scene, ora_scene, params):
+    g_img, g_hits, g_st = gpu_scene.generate_image(params, hit_ids=True, stats=True)
+    o_img, o_hits, o_st = ora_scene.render(params, mode=1, hit_ids=True)
+    r_img, r_hits, _ = ora_scene.render(params, mode=0, hit_ids=True)
+    assert np.array_equal(g_hits, o_hits), f"hit ids differ at {np.argwhere(g_hits != o_hits)[:5]}"
+    assert np.array_equal(g_hits, r_hits)
+    assert np.array_equal(g_img, o_img), f"max |d| {np.max(np.abs(g_img - o_img))}"
+    np.testing.assert_allclose(g_img, r_img, rtol=REL_TOL, atol=1e-300)
+    for k in ("paths", "segments", "aabb_tests", "tri_tests", "shape_tests", "shaded_hits",
+              "light_queries", "light_hits"):
+        assert g_st[k] == o_st[k], (k, g_st[k], o_st[k])
+    return g_img, g_hits, g_st
+
+
+def test_fp64_rounding_matches_host(rt):
+    """sqrt and division must round exactly like the host (the premise of bit-exactness)."""
+    rng = np.random.default_rng(1)
+    a = np.concatenate([rng.random(20000) * 10.0 ** rng.integers(-30, 30, 20000), [0.0, 1.0, 2.0, 1e-310, np.inf]])
+    b = np.concatenate([rng.standard_normal(20000) * 10.0 ** rng.integers(-30, 30, 20000), [1.0, 3.0, 7.0, 3.0, 2.0]])
+    assert np.array_equal(rt.probe_fp64(0, a), np.sqrt(a))
+    assert np.array_equal(rt.probe_fp64(1, a, b), a / b)
+
+
+def test_cornell_small(cornell):
+    desc, params, g, o = cornell
+    _compare(g, o, params.replace(width=48, height=40, spp=4))
+
+
+def test_cornell_seed_changes_image(cornell):
+    desc, params, g, o = cornell
+    p = params.replace(width=32, height=32, spp=2)
+    a, _, _ = g.generate_image(p)
+    b, _, _ = g.generate_image(p.replace(seed=7))
+    assert not np.array_equal(a, b)
+    a2, _, _ = g.generate_image(p)
+    assert np.array_equal(a, a2), "render must be deterministic for a fixed seed"
+
+
+def test_kitchen_sink(sink):
+    desc, params, g, o = sink
+    _compare(g, o, params)
+
+
+def test_kitchen_sink_deep(sink):
+    desc, params, g, o = sink
+    _compare(g, o, params.replace(width=24, height=20, spp=3, ray_depth=24, seed=99))
+
+
+@pytest.mark.parametrize("depth", [0, 1, 2])
+def test_shallow_depths(cornell, depth):
+    desc, params, g, o = cornell
+    _compare(g, o, params.replace(width=17, height=9, spp=2, ray_depth=depth))
+
+
+def test_one_pixel_odd_sizes(cornell):
+    desc, params, g, o = cornell
+    _compare(g, o, params.replace(width=1, height=1, spp=5))
+    _compare(g, o, params.replace(width=33, height=1, spp=1))
+    _compare(g, o, params.replace(width=1, height=31, spp=1))
+
+
+def test_fov_y_camera(cornell, rt):
+    desc, params, g, o = cornell
+    _compare(g, o, params.replace(width=20, height=30, spp=2, fov_axis=rt.RT_FOV_Y, fov=0.7))
+
+
+def test_intersect_rays_random(sink, rt):
+    desc, params, g, o = sink
+    rng = np.random.default_rng(3)
+    n = 20000
+    orig = rng.uniform(-1.2, 1.2, (n, 3))
+    d = rng.standard_normal((n, 3))
+    rays = np.concatenate([orig, d], axis=1)
+    gh, oh = g.intersect(rays), o.intersect(rays)
+    assert np.array_equal(gh["prim"], oh["prim"])
+    assert np.array_equal(gh.view(np.uint8), oh.view(np.uint8))
+
+
+def test_light_pdf_random(sink):
+    desc, params, g, o = sink
+    rng = np.random.default_rng(4)
+    n = 20000
+    pos = rng.uniform(-1.0, 1.0, (n, 3))
+    d = rng.standard_normal((n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    pd = np.concatenate([pos, d], axis=1)
+    gp, op = g.light_pdf(pd), o.light_pdf(pd)
+    assert np.array_equal(gp, op)
+    assert (gp > 0).sum() > 100
+
+
+def test_tile_partition_matches_single(cornell, rt):
+    """rt_render_tiles_async for world=3 ranks + unpack == rt_render."""
+    torch = pytest.importorskip("torch")
+    desc, params, g, o = cornell
+    p = params.replace(width=70, height=45, spp=2)
+    ref, _, _ = g.generate_image(p)
+    world = 3
+    per = g.tiles_per_rank(p, world)
+    gathered = torch.zeros((world, per, 256, 3), dtype=torch.float64, device="cuda")
+    for r in range(world):
+        g.render_tiles_async(p, r, world, gathered[r].data_ptr())
+    img = torch.zeros((p.height, p.width, 3), dtype=torch.float64, device="cuda")
+    rt.unpack_tiles_async(p, world, gathered.data_ptr(), img.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(img.cpu().numpy(), ref)
+
+
+def test_no_lights_scene(rt, orc):
+    text = """DIMENSIONS 20 16
+SAMPLES 3
+BG_COLOR 0.5 0.6 0.7
+CAMERA_POSITION 0 0 -3
+NEW_PRIMITIVE
+PLANE 0 1 0
+POSITION 0 -1 0
+COLOR 0.8 0.8 0.8
+NEW_PRIMITIVE
+ELLIPSOID 0.5 0.5 0.5
+COLOR 0.9 0.2 0.2
+"""
+    desc, params = rt.parse_scene(text)
+    _compare(rt.Scene(desc), orc.OracleScene(desc), params)
+
+
+def test_empty_scene_is_background(rt, orc):
+    desc, params = rt.parse_scene("DIMENSIONS 8 8\nSAMPLES 2\nBG_COLOR 0.25 0.5 1\n")
+    g = rt.Scene(desc)
+    img, hits, st = g.generate_image(params, hit_ids=True, stats=True)
+    assert np.all(img == np.array([0.25, 0.5, 1.0]))
+    assert np.all(hits[:, :, 0] == rt.RT_HIT_MISS) and np.all(hits[:, :, 1:] == rt.RT_HIT_NONE)
+    _compare(g, orc.OracleScene(desc), params)
