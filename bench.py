@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Msamples/s (rays traced x bounces) of the path-tracing
+hot path on the C2 workload (BASELINE.json configs[1]: Cornell box,
+1920x1080, 256 spp, depth 16) on N MI355X GPUs.
+
+One step = one full frame: every (pixel, sample) path of the frame
+(generate_image, main.rs:85-114, before tonemapping), tile-partitioned across
+the ranks (16x16 tiles round-robin), then ONE RCCL gather of the
+packed framebuffer tiles to rank 0 and the unpack into the row-major image.
+"Sample" = one path segment = one closest-hit query (raytrace.rs:14); the
+per-frame segment count is counted on the device in an untimed pass.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line.  Extras: "roofline" (canonical algorithmic bytes
+of the path kernel, DESIGN.md §4, over its HIP-event-timed launch duration)
+and "cpu_baseline" (the oracle, the C restatement of the reference, timed on
+a bounded row window of the same frame on the host cores; rank 0, N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "tests"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (import before the package: one HIP runtime per process)
+import torch.distributed as dist  # noqa: E402
+
+from conftest import load_package  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md "Chip-level parameters")
+# canonical algorithmic bytes per work unit
+B_AABB, B_TRI, B_SHAPE, B_SHADE = 32, 72, 80, 100
+
+WORKLOADS = {
+    # name: (scene file, width, height, spp, depth override or None)
+    "C2": ("cornell.txt", 1920, 1080, 256, None),
+    "C1": ("cornell.txt", 256, 256, 64, None),
+}
+
+
+def algo_bytes(st):
+    return B_AABB * st["aabb_tests"] + B_TRI * st["tri_tests"] + B_SHAPE * st["shape_tests"] + B_SHADE * st["shaded_hits"]
+
+
+def cpu_baseline(desc, params, target_s):
+    """Oracle (C restatement, kind "port") on a bounded window of rows at full spp."""
+    sys.path.insert(0, os.path.join(HERE, "oracle"))
+    import oracle as orc
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    osc = orc.OracleScene(desc)
+    mid = params.height // 2
+    # calibrate on 2 rows, then size the window for ~target_s of CPU work
+    t = time.perf_counter()
+    _, _, st = osc.render(params, mode=0, threads=threads, rows=(mid, mid + 2))
+    dt = time.perf_counter() - t
+    rows = int(max(2, min(params.height, 2 * target_s / max(dt, 1e-3))))
+    r0 = max(0, mid - rows // 2)
+    r1 = min(params.height, r0 + rows)
+    t = time.perf_counter()
+    _, _, st = osc.render(params, mode=0, threads=threads, rows=(r0, r1))
+    dt = time.perf_counter() - t
+    return {
+        "value": st["segments"] / dt / 1e6,
+        "unit": "Msamples/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"rows {r0}..{r1} of {params.width}x{params.height} at {params.spp} spp "
+                  f"({st['paths']} paths, {st['segments']} segments, {dt:.1f} s), recursive raytrace_impl, "
+                  f"OpenMP dynamic over pixels",
+        "seconds": dt,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default="C2", choices=sorted(WORKLOADS))
+    ap.add_argument("--spp", type=int, default=None, help="override spp (not the headline config)")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    rt = load_package()
+
+    scene_file, W, H, spp, depth = WORKLOADS[args.workload]
+    if args.spp:
+        spp = args.spp
+    desc, params = rt.parse_scene(open(os.path.join(HERE, "scenes", scene_file)).read())
+    params = params.replace(width=W, height=H, spp=spp, **({"ray_depth": depth} if depth else {}))
+    t0 = time.perf_counter()
+    scene = rt.Scene(desc)
+    build_s = time.perf_counter() - t0
+
+    per = scene.tiles_per_rank(params, world)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+    tiles = torch.empty((per, 256, 3), dtype=torch.float64, device=dev)
+    gathered = torch.empty((world, per, 256, 3), dtype=torch.float64, device=dev) if rank == 0 else None
+    image = torch.empty((H, W, 3), dtype=torch.float64, device=dev) if rank == 0 else None
+
+    # untimed counting pass: this rank's work of one frame
+    scene.read_stats(reset=True)
+    scene.render_tiles_async(params, rank, world, tiles.data_ptr(), sptr, stats=True)
+    st = scene.read_stats(reset=True)
+    seg = torch.tensor([st["segments"], st["paths"]], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(seg)
+    frame_segments, frame_paths = int(seg[0].item()), int(seg[1].item())
+
+    ev = []
+
+    def step(timed):
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        scene.render_tiles_async(params, rank, world, tiles.data_ptr(), sptr)
+        if timed:
+            e1.record(stream)
+            ev.append((e0, e1))
+        if world > 1:
+            dist.gather(tiles, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
+            src = gathered
+        else:
+            src = tiles
+        if rank == 0:
+            rt.unpack_tiles_async(params, world, src.data_ptr(), image.data_ptr(), sptr)
+
+    for _ in range(args.warmup):
+        step(False)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t
+    tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    elapsed = float(tt.item())
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    if rank == 0:
+        value = frame_segments * args.steps / elapsed / 1e6
+        achieved = algo_bytes(st) / (kern_ms * 1e-3) / 1e9
+        out = {
+            "metric": "Msamples/s (rays traced x bounces) at 1920x1080, 256 spp; fraction of HBM roofline",
+            "value": value,
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {
+                "workload": f"{args.workload}: Cornell box (scenes/{scene_file}, custom format, 9 primitives, "
+                            f"1 emissive box light), {W}x{H}, {spp} spp, ray_depth {params.ray_depth}",
+                "width": W, "height": H, "spp": spp, "ray_depth": params.ray_depth,
+                "paths_per_step": frame_paths, "segments_per_step": frame_segments,
+                "parallelism": f"tiles16x16 round-robin over {world} GPU(s) + 1 RCCL gather",
+                "seed": params.seed,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": None,
+                "kernel": "rt::path_kernel<false,false>",
+                "kernel_ms": kern_ms,
+                "algorithmic_bytes_per_launch": algo_bytes(st),
+                "bytes_model": "32*aabb_tests + 72*tri_tests + 80*shape_tests + 100*shaded_hits (rank 0 tiles)",
+            },
+            "paths_per_s": frame_paths * args.steps / elapsed,
+            "scene_build_s": build_s,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(desc, params, args.cpu_seconds)
+            out["speedup_vs_cpu"] = value / out["cpu_baseline"]["value"]
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -107,6 +107,7 @@ EXPORTS = {
     "rt_tiles_per_rank": (C.c_int, [C.POINTER(rt_render_params), C.c_uint32, C.POINTER(C.c_uint32)]),
     "rt_render_tiles_async": (C.c_int, [C.c_void_p, C.POINTER(rt_render_params), C.c_uint32, C.c_uint32,
                                         C.c_void_p, C.c_void_p]),
+    "rt_read_stats": (C.c_int, [C.c_void_p, C.POINTER(rt_stats), C.c_int]),
     "rt_unpack_tiles_async": (C.c_int, [C.POINTER(rt_render_params), C.c_uint32, C.c_void_p, C.c_void_p,
                                         C.c_void_p]),
     "rt_intersect_rays": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]),
@@ -389,9 +390,16 @@ class Scene:
         _check(lib().rt_tiles_per_rank(C.byref(params.to_c()), world, C.byref(n)))
         return n.value
 
-    def render_tiles_async(self, params: RenderParams, rank: int, world: int, d_out_ptr: int, stream_ptr: int = 0):
-        _check(lib().rt_render_tiles_async(self._h, C.byref(params.to_c()), rank, world, C.c_void_p(d_out_ptr),
+    def render_tiles_async(self, params: RenderParams, rank: int, world: int, d_out_ptr: int, stream_ptr: int = 0,
+                           stats: bool = False):
+        p = params.replace(flags=params.flags | (RT_FLAG_STATS if stats else 0)).to_c()
+        _check(lib().rt_render_tiles_async(self._h, C.byref(p), rank, world, C.c_void_p(d_out_ptr),
                                            C.c_void_p(stream_ptr)))
+
+    def read_stats(self, reset: bool = True) -> dict:
+        st = rt_stats()
+        _check(lib().rt_read_stats(self._h, C.byref(st), 1 if reset else 0))
+        return st.as_dict()
 
 
 def unpack_tiles_async(params: RenderParams, world: int, d_gathered_ptr: int, d_image_ptr: int, stream_ptr: int = 0):

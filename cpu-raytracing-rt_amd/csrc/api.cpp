@@ -201,6 +201,7 @@ int rt_scene_create(const rt_scene_desc* desc, rt_scene** out) {
         s->info.bvh_depth[k] = hs.bvh[k].depth;
     }
     HIP_TRY(hipMalloc(&s->d_stats, 8 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(s->d_stats, 0, 8 * sizeof(unsigned long long)));
     s->info.n_planes = d.n_planes;
     s->info.n_boxes = d.boxes.n_prims;
     s->info.n_ellipsoids = d.ells.n_prims;
@@ -239,8 +240,21 @@ int rt_render_tiles_async(rt_scene* s, const rt_render_params* p, uint32_t rank,
     KParams k = make_kparams(p, rank, world);
     uint32_t slots = slots_per_rank(k);
     if ((rc = ensure_spill(s, (uint64_t)slots * 256))) return rc;
-    HIP_TRY(launch_path(s->dev, k, slots, d_tile_rgb, nullptr, nullptr, s->spill_n, s->spill_t,
-                        (hipStream_t)stream));
+    HIP_TRY(launch_path(s->dev, k, slots, d_tile_rgb, nullptr, (p->flags & RT_FLAG_STATS) ? s->d_stats : nullptr,
+                        s->spill_n, s->spill_t, (hipStream_t)stream));
+    return RT_OK;
+}
+
+int rt_read_stats(rt_scene* s, rt_stats* out, int reset) {
+    if (!s || !out) return set_error(RT_ERR_INVALID, "scene/out is NULL");
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipDeviceSynchronize());
+    unsigned long long c[8];
+    HIP_TRY(hipMemcpy(c, s->d_stats, sizeof(c), hipMemcpyDeviceToHost));
+    std::memset(out, 0, sizeof(*out));
+    out->paths = c[0]; out->segments = c[1]; out->aabb_tests = c[2]; out->tri_tests = c[3];
+    out->shape_tests = c[4]; out->shaded_hits = c[5]; out->light_queries = c[6]; out->light_hits = c[7];
+    if (reset) HIP_TRY(hipMemset(s->d_stats, 0, sizeof(c)));
     return RT_OK;
 }
 

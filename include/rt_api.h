@@ -189,6 +189,9 @@ int rt_tiles_per_rank(const rt_render_params* params, uint32_t world, uint32_t* 
 int rt_render_tiles_async(rt_scene* scene, const rt_render_params* params,
                           uint32_t rank, uint32_t world,
                           double* d_tile_rgb, void* hip_stream);
+/* Work counters accumulated on the device by every rt_render_tiles_async call
+   made with RT_FLAG_STATS since the last reset (synchronises the device). */
+int rt_read_stats(rt_scene* scene, rt_stats* out, int reset);
 /* Root side after the gather: d_gathered = [world][n_tiles_padded][256][3]
    (rank-major, as ncclGather lays it out) -> d_image [H][W][3]. */
 int rt_unpack_tiles_async(const rt_render_params* params, uint32_t world,
