@@ -132,11 +132,7 @@ def main():
         if timed:
             e1.record(stream)
             ev.append((e0, e1))
-        if world > 1:
-            dist.gather(tiles, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
-            src = gathered
-        else:
-            src = tiles
+        src = rt.gather_tiles(tiles, gathered, rank, world)
         if rank == 0:
             rt.unpack_tiles_async(params, world, src.data_ptr(), image.data_ptr(), sptr)
 

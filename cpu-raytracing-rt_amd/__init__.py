@@ -123,6 +123,8 @@ EXPORTS = {
     "rt_api_version": (C.c_int, []),
     "rt_device_count": (C.c_int, []),
     "rt_probe_fp64": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]),
+    "rt_bvh_build": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64), C.c_void_p, C.c_void_p, C.c_void_p,
+                               C.POINTER(C.c_uint32)]),
 }
 
 _lib = None
@@ -402,6 +404,26 @@ class Scene:
         return st.as_dict()
 
 
+def tile_layout(width: int, height: int, world: int):
+    """16x16 tiles, tile t owned by rank t % world at slot t // world (DESIGN.md §5).
+    Returns (tiles_x, tiles_y, n_tiles, slots_per_rank)."""
+    tx = (width + RT_TILE - 1) // RT_TILE
+    ty = (height + RT_TILE - 1) // RT_TILE
+    n = tx * ty
+    return tx, ty, n, (n + world - 1) // world
+
+
+def gather_tiles(tiles, gathered, rank: int, world: int, group=None):
+    """The single framebuffer exchange: every rank's packed tiles [slots, 256, 3]
+    to rank 0's [world, slots, 256, 3] (rank-major, ncclGather layout) with one
+    torch.distributed gather (RCCL under the "nccl" backend, gloo on CPU)."""
+    if world == 1:
+        return tiles
+    import torch.distributed as dist
+    dist.gather(tiles, list(gathered.unbind(0)) if rank == 0 else None, dst=0, group=group)
+    return gathered
+
+
 def unpack_tiles_async(params: RenderParams, world: int, d_gathered_ptr: int, d_image_ptr: int, stream_ptr: int = 0):
     _check(lib().rt_unpack_tiles_async(C.byref(params.to_c()), world, C.c_void_p(d_gathered_ptr),
                                        C.c_void_p(d_image_ptr), C.c_void_p(stream_ptr)))
@@ -426,6 +448,22 @@ def generate_image(scene: Scene, params: RenderParams) -> np.ndarray:
     """generate_image (main.rs:85-114): tonemapped + gamma-corrected pixels."""
     img, _, _ = scene.generate_image(params)
     return tonemap_gamma(img)
+
+
+def build_bvh(boxes: np.ndarray):
+    """BVH::new over [n, 6] (min, max) boxes on the host -> (links [m,4], bounds [m,6], order [n], depth)."""
+    boxes = np.ascontiguousarray(boxes, np.float64).reshape(-1, 6)
+    n = C.c_uint64(0)
+    depth = C.c_uint32(0)
+    _check(lib().rt_bvh_build(boxes.ctypes.data_as(C.c_void_p), len(boxes), C.byref(n), None, None, None,
+                              C.byref(depth)))
+    links = np.zeros((n.value, 4), np.int64)
+    bounds = np.zeros((n.value, 6), np.float64)
+    order = np.zeros(len(boxes), np.uint64)
+    _check(lib().rt_bvh_build(boxes.ctypes.data_as(C.c_void_p), len(boxes), C.byref(n),
+                              links.ctypes.data_as(C.c_void_p), bounds.ctypes.data_as(C.c_void_p),
+                              order.ctypes.data_as(C.c_void_p), C.byref(depth)))
+    return links, bounds, order, depth.value
 
 
 def probe_fp64(op: int, a: np.ndarray, b: Optional[np.ndarray] = None) -> np.ndarray:

@@ -371,6 +371,26 @@ int rt_intersect_lights_rays(rt_scene* s, const double* rays, uint32_t n, double
     return light_query(s, rays, n, 0, out_impact, out_count);
 }
 
+int rt_bvh_build(const double* boxes, uint64_t n, uint64_t* n_nodes, int64_t* out_links, double* out_bounds,
+                 uint64_t* out_order, uint32_t* out_depth) {
+    if ((!boxes && n) || !n_nodes) return set_error(RT_ERR_INVALID, "boxes/n_nodes is NULL");
+    std::vector<Box3> b(n);
+    for (uint64_t i = 0; i < n; ++i) b[i] = Box3{load3(boxes + 6 * i), load3(boxes + 6 * i + 3)};
+    HostBvh h = build_bvh(b);
+    if (out_links && *n_nodes < h.nodes.size()) return set_error(RT_ERR_INVALID, "output too small");
+    *n_nodes = h.nodes.size();
+    if (out_depth) *out_depth = h.depth;
+    if (!out_links) return RT_OK;
+    for (size_t i = 0; i < h.nodes.size(); ++i) {
+        const HostNode& nd = h.nodes[i];
+        out_links[4 * i] = nd.left; out_links[4 * i + 1] = nd.right;
+        out_links[4 * i + 2] = (int64_t)nd.start; out_links[4 * i + 3] = (int64_t)nd.end;
+        if (out_bounds) { store3(out_bounds + 6 * i, nd.box.min); store3(out_bounds + 6 * i + 3, nd.box.max); }
+    }
+    if (out_order) for (uint64_t i = 0; i < n; ++i) out_order[i] = h.order[i];
+    return RT_OK;
+}
+
 // Diagnostic: device f64 sqrt (op 0) / division (op 1) for bit-exactness checks.
 int rt_probe_fp64(int op, const double* a, const double* b, uint32_t n, double* out) {
     if (!a || !out || (op == 1 && !b) || op < 0 || op > 1) return set_error(RT_ERR_INVALID, "bad arguments");

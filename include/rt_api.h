@@ -211,6 +211,16 @@ int rt_light_pdf_rays(rt_scene* scene, const double* pos_dir, uint32_t n, double
 int rt_intersect_lights_rays(rt_scene* scene, const double* rays, uint32_t n,
                              double* out_impact, uint32_t* out_count);
 
+/* ======================= host BVH builder ================================= */
+/* BVH::new (bvh.rs:12-17, build_nodes :75-113) over primitive boxes
+   [n][6] = (min xyz, max xyz) given in list order; host only, no device.
+   Ties of equal midpoints are broken by list index (deterministic tree).
+   Call with out_links == NULL to get *n_nodes; then with buffers of that size:
+   out_links [n_nodes][4] = (left, right, start, end) (-1: none), out_bounds
+   [n_nodes][6], out_order [n] = list index of the i-th primitive in BVH order. */
+int rt_bvh_build(const double* boxes, uint64_t n, uint64_t* n_nodes, int64_t* out_links,
+                 double* out_bounds, uint64_t* out_order, uint32_t* out_depth);
+
 /* ======================= host input surface =============================== */
 /* Custom text format (src/scene_parser.rs:5-85, defaults scene.rs:167-191). */
 int rt_parse_custom_scene(const char* text, rt_parsed_scene** out);

@@ -388,7 +388,7 @@ static void bvh_build(BVH* bvh, const AABB* boxes, uint64_t n, uint64_t* perm_ou
     bvh->nodes = b.nodes; bvh->n_nodes = b.n_nodes; bvh->depth = b.max_depth;
 }
 static void bvh_build_shapes(BVH* bvh, Shape* list, uint64_t n) {
-    AABB* boxes = (AABB*)malloc(sizeof(AABB) * (n ? n : 1));
+    AABB* boxes = (AABB*)calloc(n ? n : 1, sizeof(AABB));
     uint64_t* perm = (uint64_t*)malloc(sizeof(uint64_t) * (n ? n : 1));
     for (uint64_t i = 0; i < n; ++i) boxes[i] = list[i].aabb;
     bvh_build(bvh, boxes, n, perm);
@@ -398,7 +398,7 @@ static void bvh_build_shapes(BVH* bvh, Shape* list, uint64_t n) {
     free(boxes); free(perm);
 }
 static void bvh_build_tris(BVH* bvh, Tri* list, uint64_t n) {
-    AABB* boxes = (AABB*)malloc(sizeof(AABB) * (n ? n : 1));
+    AABB* boxes = (AABB*)calloc(n ? n : 1, sizeof(AABB));
     uint64_t* perm = (uint64_t*)malloc(sizeof(uint64_t) * (n ? n : 1));
     for (uint64_t i = 0; i < n; ++i) boxes[i] = list[i].aabb;
     bvh_build(bvh, boxes, n, perm);
@@ -1179,5 +1179,43 @@ void oracle_ppm_bytes(const double* rgb, uint64_t n, uint8_t* out) { /* ppm.rs:1
         if (v > 1.0) v = 1.0; /* f64::clamp */
         double r = round(v * 255.0);
         out[i] = (uint8_t)(r != r ? 0 : r); /* `as u8` saturates, NaN -> 0 */
+    }
+}
+
+/* ======================================================================= */
+/* extra hooks: raw BVH build, raw intersect_lights                         */
+/* ======================================================================= */
+uint64_t oracle_bvh_build(const double* boxes, uint64_t n, int64_t* links, double* bounds, uint64_t* order,
+                          uint32_t* depth) {
+    AABB* bx = (AABB*)malloc(sizeof(AABB) * (n ? n : 1));
+    for (uint64_t i = 0; i < n; ++i) { bx[i].min = vld(boxes + 6 * i); bx[i].max = vld(boxes + 6 * i + 3); }
+    uint64_t* perm = (uint64_t*)malloc(sizeof(uint64_t) * (n ? n : 1));
+    BVH b;
+    bvh_build(&b, bx, n, perm);
+    if (links) {
+        for (uint64_t i = 0; i < b.n_nodes; ++i) {
+            const Node* nd = &b.nodes[i];
+            links[4 * i + 0] = nd->left; links[4 * i + 1] = nd->right;
+            links[4 * i + 2] = (int64_t)nd->start; links[4 * i + 3] = (int64_t)nd->end;
+            if (bounds) { vst(bounds + 6 * i, nd->aabb.min); vst(bounds + 6 * i + 3, nd->aabb.max); }
+        }
+        if (order) for (uint64_t i = 0; i < n; ++i) order[i] = perm[i];
+    }
+    if (depth) *depth = b.depth;
+    uint64_t nn = b.n_nodes;
+    free(b.nodes); free(bx); free(perm);
+    return nn;
+}
+void oracle_intersect_lights_rays(const oracle_scene* s, const double* rays, uint32_t n, double* impact,
+                                  uint32_t* count) {
+    for (uint32_t i = 0; i < n; ++i) {
+        Counters c = {0};
+        PdfAcc acc = {0.0, vld(rays + 6 * i + 3), &c};
+        V3 o = vld(rays + 6 * i), d = vld(rays + 6 * i + 3);
+        bvh_all(&s->lboxes, o, d, &acc); /* intersections.rs:87-91 */
+        bvh_all(&s->lells, o, d, &acc);
+        bvh_all(&s->ltris, o, d, &acc);
+        impact[i] = acc.impact;
+        if (count) count[i] = (uint32_t)c.lhits;
     }
 }

@@ -81,6 +81,13 @@ void oracle_rng_stream_u64(uint64_t seed, uint64_t pixel, uint32_t sample, uint3
 void oracle_sampler_draws(uint64_t seed, uint64_t pixel, uint32_t sample, int kind,
                           const double arg[3], uint32_t n, double* out);
 
+/* BVH::new over raw boxes [n][6]; returns node count (call with links NULL first). */
+uint64_t oracle_bvh_build(const double* boxes, uint64_t n, int64_t* links, double* bounds, uint64_t* order,
+                          uint32_t* depth);
+/* intersect_lights accumulation without offset/normalisation + callback count. */
+void oracle_intersect_lights_rays(const oracle_scene* s, const double* rays, uint32_t n, double* impact,
+                                  uint32_t* count);
+
 /* ---- host output surface restated (postprocessing.rs, ppm.rs) ----------- */
 void oracle_tonemap_gamma(const double* in, uint64_t n_pixels, double* out);
 void oracle_ppm_bytes(const double* rgb, uint64_t n_pixels, uint8_t* out);

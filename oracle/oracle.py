@@ -50,6 +50,8 @@ def lib():
             "oracle_sampler_draws": (None, [u64, u64, u32, i32, dp, u32, dp]),
             "oracle_tonemap_gamma": (None, [vp, u64, vp]),
             "oracle_ppm_bytes": (None, [vp, u64, vp]),
+            "oracle_bvh_build": (u64, [vp, u64, vp, vp, vp, vp]),
+            "oracle_intersect_lights_rays": (None, [vp, vp, u32, vp, vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -125,6 +127,13 @@ class OracleScene:
         lib().oracle_intersect_rays(self._h, rays.ctypes.data, len(rays), out.ctypes.data)
         return out
 
+    def intersect_lights(self, rays):
+        rays = np.ascontiguousarray(rays, np.float64).reshape(-1, 6)
+        imp = np.zeros(len(rays), np.float64)
+        cnt = np.zeros(len(rays), np.uint32)
+        lib().oracle_intersect_lights_rays(self._h, rays.ctypes.data, len(rays), imp.ctypes.data, cnt.ctypes.data)
+        return imp, cnt
+
     def light_pdf(self, pos_dir):
         pos_dir = np.ascontiguousarray(pos_dir, np.float64).reshape(-1, 6)
         out = np.zeros(len(pos_dir), np.float64)
@@ -143,6 +152,19 @@ def _stats_struct():
                     ("light_queries", C.c_uint64), ("light_hits", C.c_uint64), ("kernel_ms", C.c_double),
                     ("total_ms", C.c_double)]
     return rt_stats()
+
+
+def build_bvh(boxes):
+    """BVH::new over [n, 6] boxes -> (links [m,4], bounds [m,6], order [n], depth)."""
+    boxes = np.ascontiguousarray(boxes, np.float64).reshape(-1, 6)
+    m = int(lib().oracle_bvh_build(boxes.ctypes.data, len(boxes), None, None, None, None))
+    links = np.zeros((m, 4), np.int64)
+    bounds = np.zeros((m, 6), np.float64)
+    order = np.zeros(len(boxes), np.uint64)
+    depth = np.zeros(1, np.uint32)
+    lib().oracle_bvh_build(boxes.ctypes.data, len(boxes), links.ctypes.data, bounds.ctypes.data, order.ctypes.data,
+                           depth.ctypes.data)
+    return links, bounds, order, int(depth[0])
 
 
 # ----------------------------------------------------------- KAT hooks ----

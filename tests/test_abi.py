@@ -1,0 +1,148 @@
+"""CPU tests of the product library (no device calls): every symbol the C ABI
+header declares is exported, the host-side pieces (custom-scene parser, BVH
+builder, ACES/gamma/PPM output surface) match the oracle / the reference's
+rules, and the hot path refuses to run without a GPU (no CPU fallback)."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "rt_api.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rt_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_symbols_exported(rt):
+    import ctypes
+    lib = ctypes.CDLL(rt.LIB_PATH)
+    names = declared_functions()
+    assert len(names) >= 20
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    assert set(names) == set(rt.EXPORTS), set(names) ^ set(rt.EXPORTS)
+
+
+def test_version_and_errors(rt):
+    assert rt.lib().rt_api_version() == 1
+    with pytest.raises(rt.RtError) as e:
+        rt.parse_scene("NEW_PRIMITIVE\nBOX 1 2\n")
+    assert e.value.code == -4
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="a GPU is visible")
+def test_no_cpu_fallback(rt, scene_text):
+    assert rt.device_count() == 0
+    desc, params = rt.parse_scene(scene_text("cornell.txt"))
+    with pytest.raises(rt.RtError) as e:
+        rt.Scene(desc)
+    assert e.value.code == -2 and "no HIP device" in str(e.value)
+
+
+# ------------------------------------------------------------- parser ----
+def test_parse_cornell(rt, scene_text):
+    desc, p = rt.parse_scene(scene_text("cornell.txt"))
+    assert (p.width, p.height, p.spp, p.ray_depth) == (256, 256, 64, 16)
+    assert p.fov == 0.9 and p.fov_axis == rt.RT_FOV_X
+    assert list(desc.shapes["type"]) == [0, 0, 0, 0, 0, 1, 1, 2, 2]
+    assert list(desc.materials["kind"]) == [0, 0, 0, 0, 0, 0, 0, 2, 1]
+    assert desc.materials["ior"][7] == 1.5
+    assert list(desc.materials["emission"][5]) == [10, 10, 10]
+    # ROTATION x y z w -> (s, x, y, z) = (w, x, y, z) (scene_parser.rs:51-57)
+    assert list(desc.shapes["rotation"][6]) == [0.984807753012208, 0, 0.17364817766693033, 0]
+    assert list(desc.shapes["rotation"][0]) == [1, 0, 0, 0]
+
+
+def test_parse_defaults(rt):
+    """Scene::new / CameraParams::new defaults (scene.rs:167-191)."""
+    desc, p = rt.parse_scene("DIMENSIONS 3 2\nCAMERA_FORWARD 0 0 2\nCAMERA_UP 0 3 0\n")
+    assert (p.spp, p.ray_depth, p.bg_color) == (64, 16, (0.0, 0.0, 0.0))
+    assert p.cam_forward == (0.0, 0.0, 1.0) and p.cam_up == (0.0, 1.0, 0.0)  # normalised
+    assert p.fov == np.pi / 2 and p.cam_position == (0.0, 0.0, 0.0)
+    assert len(desc.shapes) == 0 and len(desc.tri_material) == 0
+
+
+def test_parse_ignores_unknown_and_blank(rt):
+    desc, p = rt.parse_scene("garbage line\n\n  \nDIMENSIONS 4 4\nWHATEVER 1 2 3\nNEW_PRIMITIVE\nPLANE 0 1 0\n")
+    assert len(desc.shapes) == 1
+
+
+def test_parse_triangles_and_props(rt):
+    text = ("DIMENSIONS 8 8\nNEW_PRIMITIVE\nTRIANGLE 0 0 0 1 0 0 0 1 0\nPOSITION 1 2 3\n"
+            "ROTATION 0 0 0.5 0.5\nCOLOR 0.1 0.2 0.3\nMETALLIC\nRAY_DEPTH 3\nSAMPLES 5\nBG_COLOR 1 1 1\n")
+    desc, p = rt.parse_scene(text)
+    assert p.ray_depth == 3 and p.spp == 5 and p.bg_color == (1.0, 1.0, 1.0)
+    assert list(desc.tri_vertices[0]) == [0, 0, 0, 1, 0, 0, 0, 1, 0]
+    assert list(desc.tri_position[0]) == [1, 2, 3]
+    assert list(desc.tri_rotation[0]) == [0.5, 0, 0, 0.5]
+    assert desc.materials["kind"][0] == rt.RT_MAT_METALLIC
+
+
+@pytest.mark.parametrize("text", [
+    "NEW_PRIMITIVE\nPLANE 0 1 0\n",                           # no DIMENSIONS (scene.rs:188 unwrap)
+    "DIMENSIONS 4 4\nPLANE 0 1 0\n",                          # property before NEW_PRIMITIVE
+    "DIMENSIONS 4 4\nNEW_PRIMITIVE\nCOLOR 1 1 1\n",           # primitive without shape
+    "DIMENSIONS 4 4\nNEW_PRIMITIVE\nBOX 1 1 1\nDIELECTRIC\n",  # DIELECTRIC without IOR
+    "DIMENSIONS 4 4\nNEW_PRIMITIVE\nBOX 1 x 1\n",             # f64 parse error
+    "DIMENSIONS 4\n",                                         # missing token
+    "DIMENSIONS 4 4\nRAY_DEPTH 300\n",                        # u8 overflow
+])
+def test_parse_errors(rt, text):
+    with pytest.raises(rt.RtError) as e:
+        rt.parse_scene(text)
+    assert e.value.code == -4
+
+
+# --------------------------------------------------------- BVH builder ----
+def _boxes(rng, n, grid=False):
+    c = rng.integers(0, 4, (n, 3)).astype(float) if grid else rng.uniform(-10, 10, (n, 3))
+    h = rng.uniform(0.01, 1.0, (n, 3))
+    return np.concatenate([c - h, c + h], axis=1)
+
+
+@pytest.mark.parametrize("n,grid", [(1, False), (4, False), (5, False), (37, False), (500, False),
+                                    (300, True), (2000, True)])
+def test_bvh_builder_matches_oracle(rt, orc, n, grid):
+    """Product builder == oracle builder node for node (bvh.rs:75-140), incl. equal-midpoint ties."""
+    boxes = _boxes(np.random.default_rng(n), n, grid)
+    a = rt.build_bvh(boxes)
+    b = orc.build_bvh(boxes)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
+    assert a[3] == b[3]
+    links = a[0]
+    leaves = links[links[:, 0] < 0]
+    assert (leaves[:, 3] - leaves[:, 2]).sum() == n  # every primitive in exactly one leaf
+    assert sorted(a[2].tolist()) == list(range(n))
+
+
+def test_bvh_same_boxes_is_one_leaf(rt):
+    """SAH finds no gain on identical boxes -> one leaf holding all of them (bvh.rs:93-96)."""
+    boxes = np.tile([0, 0, 0, 1, 1, 1.0], (9, 1))
+    links, bounds, order, depth = rt.build_bvh(boxes)
+    assert len(links) == 1 and links[0, 3] == 9 and depth == 1
+
+
+# ---------------------------------------------------- output surface ----
+def test_tonemap_gamma_matches_oracle(rt, orc):
+    x = np.random.default_rng(0).uniform(-1, 30, (64, 3))
+    x[0] = [0.0, np.nan, np.inf]
+    a, b = rt.tonemap_gamma(x), orc.tonemap_gamma(x)
+    assert np.array_equal(a, b, equal_nan=True)
+
+
+def test_ppm_writer(rt, orc, tmp_path):
+    rgb = np.random.default_rng(1).uniform(-0.2, 1.2, (5, 7, 3))
+    rgb[0, 0] = [0.5 / 255, 1.5 / 255, np.nan]  # round half away from zero; NaN -> 0
+    path = str(tmp_path / "x.ppm")
+    rt.save_to_ppm(path, rgb)
+    data = open(path, "rb").read()
+    head = b"P6\n7 5\n255\n"
+    assert data.startswith(head)
+    assert np.array_equal(np.frombuffer(data[len(head):], np.uint8), orc.ppm_bytes(rgb))
+    assert list(data[len(head):len(head) + 3]) == [1, 2, 0]

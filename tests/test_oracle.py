@@ -1,0 +1,202 @@
+"""CPU tests of the oracle (oracle/oracle.c): pinned against the reference's own
+known-answer tests (tests/golden/kats.json), internally consistent (recursive
+raytrace_impl vs the device's throughput form), and reproducing the committed
+golden fixtures."""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+GOLD = os.path.join(REPO, "tests", "golden")
+with open(os.path.join(GOLD, "kats.json")) as f:
+    KATS = json.load(f)
+
+
+def cg_normalize(v):
+    """cgmath normalize: v * (1 / sqrt((x*x + y*y) + z*z))."""
+    x, y, z = (float(c) for c in v)
+    inv = 1.0 / math.sqrt((x * x + y * y) + z * z)
+    return [x * inv, y * inv, z * inv]
+
+
+# ---------------------------------------------------------------- KATs ----
+@pytest.mark.parametrize("kat", KATS["aabb"], ids=lambda k: k["name"])
+def test_kat_aabb(orc, kat):
+    d = cg_normalize(kat["dir"]) if kat["normalize"] else kat["dir"]
+    t = orc.aabb_intersects(kat["min"], kat["max"], kat["origin"], d)
+    assert t == kat["expected_t"]  # exact, as the reference's assert_eq!
+
+
+@pytest.mark.parametrize("kat", KATS["box"], ids=lambda k: k["name"])
+def test_kat_box(orc, kat):
+    d = cg_normalize(kat["dir"])
+    r = orc.box_intersection(kat["sizes"], kat["origin"], d)
+    exp = kat["expected"]
+    if exp is None:
+        assert r is None
+    else:
+        t, n, inside = r
+        assert t == exp["t"] and list(n) == exp["normal"] and inside == exp["inside"]
+
+
+def test_kat_triangle_bbb(orc):
+    k = KATS["triangle_bbb"]
+    r = orc.triangle_intersection(k["a"] + k["b"] + k["c"], [0, 0, 0], [1, 0, 0, 0], k["origin"], k["dir"])
+    assert r is None  # |det| < 1e-11 (triangle.rs:51)
+
+
+def triangle_aaa_scene(rt):
+    k = KATS["triangle_aaa"]
+    a, ba, ca = (np.array(k[x]) for x in ("a", "ba", "ca"))
+    mats = np.zeros(1, rt.MATERIAL_DTYPE)
+    mats[0]["emission"] = (1.0, 1.0, 1.0)
+    desc = rt.SceneDesc(materials=mats, shapes=np.zeros(0, rt.SHAPE_DTYPE),
+                        tri_vertices=np.concatenate([a, a + ba, a + ca])[None, :],
+                        tri_position=np.array([k["position"]]), tri_rotation=np.array([[1.0, 0, 0, 0]]),
+                        tri_material=np.zeros(1, np.uint32))
+    # TrianglePrimitive::new with no rotation: a' = a + pos; ba', ca' recomputed from b', c'
+    pos = np.array(k["position"])
+    a2 = a + pos
+    b2 = (ba + a) + pos
+    c2 = (ca + a) + pos
+    ba2, ca2 = b2 - a2, c2 - a2
+    world = (ba2 * k["u"] + ca2 * k["v"]) + a2
+    o = np.array(k["pos"])
+    d = np.array(cg_normalize(world + o))
+    return desc, np.concatenate([o, d])[None, :]
+
+
+def test_kat_triangle_aaa(rt, orc):
+    desc, ray = triangle_aaa_scene(rt)
+    imp, cnt = orc.OracleScene(desc).intersect_lights(ray)
+    assert cnt[0] >= 1  # `called` (primitives/triangle.rs:125-127)
+
+
+def test_kat_cof_aaa(orc):
+    """cof(M)·n ∥ (Mᵀ)⁻¹·n for M = Rx(10°)·Ry(20°)·Rz(30°)·diag(2,3,4) (gltf/scene_builder.rs:408-426)."""
+    k = KATS["cof_aaa"]
+
+    def rx(t):  # cgmath Matrix3::from_angle_x, columns
+        s, c = math.sin(t), math.cos(t)
+        return np.array([[1, 0, 0], [0, c, s], [0, -s, c]]).T
+
+    def ry(t):
+        s, c = math.sin(t), math.cos(t)
+        return np.array([[c, 0, -s], [0, 1, 0], [s, 0, c]]).T
+
+    def rz(t):
+        s, c = math.sin(t), math.cos(t)
+        return np.array([[c, s, 0], [-s, c, 0], [0, 0, 1]]).T
+
+    ang = [a * (math.pi / 180.0) for a in k["angles_deg"]]
+    m = rx(ang[0]) @ ry(ang[1]) @ rz(ang[2]) @ np.diag(k["scales"])
+    cof = orc.cof3(m.T.reshape(9)).reshape(3, 3).T  # column-major in/out
+    inv_t = np.linalg.inv(m.T)
+    for n in k["normals"]:
+        n = np.array(cg_normalize(n))
+        a = cof @ n
+        b = inv_t @ n
+        np.testing.assert_allclose(a / np.linalg.norm(a), b / np.linalg.norm(b), atol=1e-15)
+
+
+@pytest.mark.parametrize("v", KATS["philox4x32_10"], ids=["zero", "ones", "pi"])
+def test_kat_philox(orc, v):
+    assert list(orc.philox(v["ctr"], v["key"])) == v["out"]
+
+
+# ------------------------------------------------------ sampler sanity ----
+def test_rand_transforms(orc):
+    seed = 1234
+    # gen_range(0..n): uniform over n values
+    draws = np.concatenate([orc.sampler_draws(seed, p, 0, 3, [5, 0, 0], 200)[:, 0] for p in range(20)])
+    counts = np.bincount(draws.astype(int), minlength=5)
+    assert counts.sum() == 4000 and counts.min() > 700
+    # gen_bool(0.5)
+    b = np.concatenate([orc.sampler_draws(seed, p, 1, 4, [0.5, 0, 0], 200)[:, 0] for p in range(20)])
+    assert 1800 < b.sum() < 2200
+    assert np.all(orc.sampler_draws(seed, 0, 0, 4, [1.0, 0, 0], 50)[:, 0] == 1)  # p == 1: ALWAYS_TRUE
+    assert np.all(orc.sampler_draws(seed, 0, 0, 4, [0.0, 0, 0], 50)[:, 0] == 0)
+    # inclusive [-1, 1] and half-open [0, 3)
+    u = orc.sampler_draws(seed, 3, 0, 5, [-1.0, 1.0, 0], 2000)[:, 0]
+    assert u.min() >= -1.0 and u.max() <= 1.0 and abs(u.mean()) < 0.08
+    h = orc.sampler_draws(seed, 4, 0, 6, [0.0, 3.0, 0], 2000)[:, 0]
+    assert h.min() >= 0.0 and h.max() < 3.0
+
+
+def test_samplers_geometry(orc):
+    s = np.array([0.25, 0.01, 0.5])
+    pts = orc.sampler_draws(7, 0, 0, 1, s, 3000)
+    on_face = np.isclose(np.abs(pts) / s, 1.0, rtol=0, atol=1e-15).any(axis=1)
+    assert on_face.all() and (np.abs(pts) <= s + 1e-15).all()
+    # faces chosen proportional to (sy*sz, sx*sz, sx*sy)
+    face = np.argmax(np.isclose(np.abs(pts) / s, 1.0, rtol=0, atol=1e-15), axis=1)
+    w = np.array([s[1] * s[2], s[0] * s[2], s[0] * s[1]])
+    np.testing.assert_allclose(np.bincount(face, minlength=3) / len(face), w / w.sum(), atol=0.03)
+    sph = orc.sampler_draws(7, 1, 0, 2, [0, 0, 0], 2000)
+    np.testing.assert_allclose(np.linalg.norm(sph, axis=1), 1.0, atol=1e-15)
+    n = np.array([0.0, 1.0, 0.0])
+    cos = orc.sampler_draws(7, 2, 0, 0, n, 4000)
+    np.testing.assert_allclose(np.linalg.norm(cos, axis=1), 1.0, atol=1e-15)
+    assert (cos @ n > 0).mean() > 0.99
+
+
+# -------------------------------------------- recursive vs device form ----
+@pytest.mark.parametrize("scene,over", [
+    ("cornell.txt", dict(width=32, height=24, spp=4)),
+    ("kitchen_sink.txt", {}),
+    ("kitchen_sink.txt", dict(width=16, height=12, spp=3, ray_depth=30, seed=5)),
+])
+def test_recursive_vs_iterative(rt, orc, scene_text, scene, over):
+    desc, params = rt.parse_scene(scene_text(scene))
+    params = params.replace(**over)
+    o = orc.OracleScene(desc)
+    a, ha, sa = o.render(params, mode=0, hit_ids=True)
+    b, hb, sb = o.render(params, mode=1, hit_ids=True)
+    assert np.array_equal(ha, hb)
+    np.testing.assert_allclose(a, b, rtol=1e-12, atol=1e-300)
+    for k in ("paths", "segments", "aabb_tests", "tri_tests", "shape_tests", "shaded_hits",
+              "light_queries", "light_hits"):
+        assert sa[k] == sb[k]
+
+
+def test_thread_count_independent(rt, orc, scene_text):
+    desc, params = rt.parse_scene(scene_text("kitchen_sink.txt"))
+    o = orc.OracleScene(desc)
+    a, ha, _ = o.render(params, threads=1, hit_ids=True)
+    b, hb, _ = o.render(params, threads=7, hit_ids=True)
+    assert np.array_equal(a, b) and np.array_equal(ha, hb)
+
+
+def test_row_window_matches_full(rt, orc, scene_text):
+    desc, params = rt.parse_scene(scene_text("kitchen_sink.txt"))
+    o = orc.OracleScene(desc)
+    full, _, _ = o.render(params)
+    part, _, st = o.render(params, rows=(10, 17))
+    assert np.array_equal(full[10:17], part[10:17]) and st["paths"] == 7 * params.width * params.spp
+
+
+@pytest.mark.parametrize("name", ["cornell_24x16_4spp", "kitchen_sink", "kitchen_sink_deep"])
+def test_golden_fixtures(orc, name):
+    import sys
+    sys.path.insert(0, GOLD)
+    from make_golden import render_case
+    g = np.load(os.path.join(GOLD, name + ".npz"))
+    params, img, hits, stats = render_case(name)
+    assert np.array_equal(img, g["image"])
+    assert np.array_equal(hits, g["hit_ids"])
+    assert np.array_equal(stats, g["stats"])
+
+
+def test_light_scene_bvhs(rt, orc, scene_text):
+    desc, params = rt.parse_scene(scene_text("kitchen_sink.txt"))
+    o = orc.OracleScene(desc)
+    nodes, depth = o.bvh_info()
+    # 5 boxes and 6 ellipsoids need a split; the 4 triangles fit one leaf (bvh.rs:77)
+    assert nodes[0] > 1 and nodes[1] > 1 and nodes[2] == 1
+    # lights are copies in their own BVHs (scene.rs:209-213): 1 box, 1 ellipsoid, 1 triangle
+    assert list(nodes[3:]) == [1, 1, 1]
+    assert sorted(o.bvh_prims(3) + o.bvh_prims(4) + o.bvh_prims(5)) == [2, 3, 13]
