@@ -32,7 +32,8 @@ from typing import Optional
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "build", "librt_amd.so")
+# RT_AMD_LIB: alternate build of the same library (tuning experiments only)
+LIB_PATH = os.environ.get("RT_AMD_LIB") or os.path.join(_HERE, "build", "librt_amd.so")
 
 # ----------------------------------------------------------------- ABI ----
 RT_MAT_DIFFUSE, RT_MAT_METALLIC, RT_MAT_DIELECTRIC = 0, 1, 2

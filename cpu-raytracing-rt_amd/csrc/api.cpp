@@ -109,6 +109,7 @@ KParams make_kparams(const rt_render_params* p, uint32_t rank, uint32_t world) {
     std::memset(&k, 0, sizeof(k));
     k.width = p->width; k.height = p->height; k.spp = p->spp; k.ray_depth = p->ray_depth;
     k.fw = (double)p->width; k.fh = (double)p->height;
+    k.inv_fw = 1.0 / k.fw; k.inv_fh = 1.0 / k.fh;
     if (p->fov_axis == RT_FOV_Y) {
         k.tan_y = std::tan(p->fov / 2.0);
         double aspect = k.fh / k.fw;

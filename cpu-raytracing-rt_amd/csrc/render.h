@@ -14,6 +14,7 @@ namespace rt {
 struct KParams {
     uint32_t width, height, spp, ray_depth;
     double fw, fh, tan_x, tan_y;
+    double inv_fw, inv_fh;     // RN(1/fw), RN(1/fh) for the exact reciprocal division
     double cam_pos[3], cam_right[3], cam_up[3], cam_fwd[3];
     double bg[3];
     double scale01, scale11;   // UniformFloat::new_inclusive scales for [0,1], [-1,1]

@@ -25,6 +25,9 @@
 namespace rt {
 
 constexpr int kBlock = 256;
+#ifndef RT_MIN_WAVES
+#define RT_MIN_WAVES 3  // path_kernel register budget: 3 waves/SIMD measured best
+#endif
 constexpr int kShort = kMaxBvhDepthShort;
 
 // ---------------------------------------------------------------- stack ---
@@ -59,19 +62,19 @@ struct Cand {
 
 // closest hit of one shape in model space; t + aux
 template <int KIND>
-RT_D bool shape_closest(const DevShape& s, V3 o, V3 d, double& t, uint32_t& aux) {
+RT_D bool shape_closest(const DevShape& s, V3 o, V3 d, const Rcp3& rc, double& t, uint32_t& aux) {
     V3 mo, md;
-    model_ray(s, o, d, mo, md);
+    const bool same = model_ray(s, o, d, mo, md);
     if (KIND == 0) return plane_t(load3(s.shape), mo, md, t, aux);
     if (KIND == 1) {
         Bpi en, ex;
-        int k = box_coef(load3(s.shape), mo, md, en, ex);
+        int k = box_coef(load3(s.shape), mo, md, same ? rc : make_rcp3(md), en, ex);
         if (k == 2) { t = en.t; aux = bpi_aux(en, false); return true; }
         if (k == 1) { t = ex.t; aux = bpi_aux(ex, true); return true; }
         return false;
     }
     double t1, t2;
-    int k = ell_coef(load3(s.shape), mo, md, t1, t2);
+    int k = ell_coef(load_radii(s), mo, md, t1, t2);
     if (k == 2) { t = t1; aux = 0; return true; }
     if (k == 1) { t = t2; aux = 8; return true; }
     return false;
@@ -79,12 +82,12 @@ RT_D bool shape_closest(const DevShape& s, V3 o, V3 d, double& t, uint32_t& aux)
 
 // BVH::intersection (bvh.rs:27-36) + Node::intersection (bvh.rs:151-186)
 template <int KIND, bool ST>
-RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, Stack& S, Cnt<ST>& C, double& bt_out, double& bu,
-                      double& bv, uint32_t& bprim, uint32_t& baux) {
+RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stack& S, Cnt<ST>& C, double& bt_out,
+                      double& bu, double& bv, uint32_t& bprim, uint32_t& baux) {
     if (B.n_prims == 0) return false;
     double t0;
     C.aabb();
-    if (!aabb_hit(load3(B.root_min), load3(B.root_max), o, d, t0)) return false;
+    if (!aabb_hit(load3(B.root_min), load3(B.root_max), o, d, rc, t0)) return false;
     bool valid = false;
     double best = INFINITY;
     uint32_t node = 0;
@@ -97,7 +100,7 @@ RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, Stack& S, Cnt<ST>& C, double&
             uint32_t aux = 0;
             bool h;
             if (KIND == 3) { C.tri(); h = tri_uvt(B.tris[i], o, d, u, v, t); }
-            else { C.shape(); h = shape_closest<KIND>(B.shapes[i], o, d, t, aux); }
+            else { C.shape(); h = shape_closest<KIND>(B.shapes[i], o, d, rc, t, aux); }
             if (h && (!valid || t < best)) {  // update_best_intersection (bvh.rs:213-222)
                 valid = true; best = t; bu = u; bv = v; bprim = i; baux = aux;
             }
@@ -106,8 +109,8 @@ RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, Stack& S, Cnt<ST>& C, double&
         if (left >= 0) {
             double lt = 0.0, rt2 = 0.0;
             C.aabb(2);
-            bool lh = aabb_hit(load3(n.lmin), load3(n.lmax), o, d, lt);
-            bool rh = aabb_hit(load3(n.rmin), load3(n.rmax), o, d, rt2);
+            bool lh = aabb_hit(load3(n.lmin), load3(n.lmax), o, d, rc, lt);
+            bool rh = aabb_hit(load3(n.rmin), load3(n.rmax), o, d, rc, rt2);
             const double bt = best;  // +inf when no hit yet
             const double li = lh ? (lt < bt ? lt : bt) : bt;
             const double ri = rh ? (rt2 < bt ? rt2 : bt) : bt;
@@ -166,7 +169,7 @@ RT_D Hit materialise(const DevScene& S, const Cand& c, V3 o, V3 d, Quat& rot, ui
     } else {
         V3 mo, md;
         model_ray(s, o, d, mo, md);
-        V3 n = ell_normal(load3(s.shape), mo, md, c.t);
+        V3 n = ell_normal(load_radii(s), mo, md, c.t);
         bool inside = (c.aux & 8u) != 0;
         if (inside) n = -n;
         h.ng = n; h.ns = n; h.inside = inside;
@@ -180,27 +183,28 @@ RT_D bool scene_intersect(const DevScene& S, V3 o, V3 d, Stack& stk, Cnt<ST>& C,
                           int32_t& gid) {
     Cand best;
     best.valid = false; best.t = 0.0; best.u = best.v = 0.0; best.prim = 0; best.aux = 0; best.kind = 0;
+    const Rcp3 rc = make_rcp3(d);  // dead (DCE'd) unless RT_FASTDIV
     for (uint32_t i = 0; i < S.n_planes; ++i) {  // :45-49
         double t; uint32_t aux;
         C.shape();
-        if (!shape_closest<0>(S.planes[i], o, d, t, aux)) continue;
+        if (!shape_closest<0>(S.planes[i], o, d, rc, t, aux)) continue;
         if (!best.valid || t < best.t) { best.valid = true; best.t = t; best.prim = i; best.aux = aux; best.kind = 0; }
     }
     {
         double t, u, v; uint32_t p, aux = 0;
-        if (bvh_closest<1, ST>(S.boxes, o, d, stk, C, t, u, v, p, aux) && (!best.valid || t < best.t)) {
+        if (bvh_closest<1, ST>(S.boxes, o, d, rc, stk, C, t, u, v, p, aux) && (!best.valid || t < best.t)) {
             best.valid = true; best.t = t; best.prim = p; best.aux = aux; best.kind = 1;
         }
     }
     {
         double t, u, v; uint32_t p, aux = 0;
-        if (bvh_closest<2, ST>(S.ells, o, d, stk, C, t, u, v, p, aux) && (!best.valid || t < best.t)) {
+        if (bvh_closest<2, ST>(S.ells, o, d, rc, stk, C, t, u, v, p, aux) && (!best.valid || t < best.t)) {
             best.valid = true; best.t = t; best.prim = p; best.aux = aux; best.kind = 2;
         }
     }
     {
         double t, u = 0.0, v = 0.0; uint32_t p, aux = 0;
-        if (bvh_closest<3, ST>(S.tris, o, d, stk, C, t, u, v, p, aux) && (!best.valid || t < best.t)) {
+        if (bvh_closest<3, ST>(S.tris, o, d, rc, stk, C, t, u, v, p, aux) && (!best.valid || t < best.t)) {
             best.valid = true; best.t = t; best.prim = p; best.u = u; best.v = v; best.aux = 0; best.kind = 3;
         }
     }
@@ -215,7 +219,7 @@ RT_D bool scene_intersect(const DevScene& S, V3 o, V3 d, Stack& stk, Cnt<ST>& C,
 
 // ---------------------------------------------------------- light pdf ----
 // intersection_probability.rs:9-35 + to_direction_probability (ray_sampler.rs:172-174)
-RT_D double prob_box(V3 s) { return 1.0 / ((s.y * s.z + s.x * s.z) + s.x * s.y) / 8.0; }
+// (the box's 1/sum/8 is a per-primitive constant precomputed on the host: DevShape::aux[0])
 RT_D double prob_ell(V3 r, V3 ng) {
     V3 coef = mul(v3(r.y * r.z, r.x * r.z, r.x * r.y), ng);
     return 1.0 / (4.0 * kPi * sqrt(dot(coef, coef)));
@@ -223,11 +227,12 @@ RT_D double prob_ell(V3 r, V3 ng) {
 
 // Node::intersections (bvh.rs:188-210) accumulating the Light::pdf callback
 template <int KIND, bool ST>
-RT_D void bvh_all(const DevBvh& B, V3 o, V3 d, Stack& S, Cnt<ST>& C, double& impact, uint32_t& nhits) {
+RT_D void bvh_all(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stack& S, Cnt<ST>& C, double& impact,
+                  uint32_t& nhits) {
     if (B.n_prims == 0) return;
     double t0;
     C.aabb();
-    if (!aabb_hit(load3(B.root_min), load3(B.root_max), o, d, t0)) return;
+    if (!aabb_hit(load3(B.root_min), load3(B.root_max), o, d, rc, t0)) return;
     uint32_t node = 0;
     S.sp = 0;
     for (;;) {
@@ -246,13 +251,14 @@ RT_D void bvh_all(const DevBvh& B, V3 o, V3 d, Stack& S, Cnt<ST>& C, double& imp
                 C.shape();
                 const DevShape s = B.shapes[i];
                 V3 mo, md;
-                model_ray(s, o, d, mo, md);
+                const bool same = model_ray(s, o, d, mo, md);
                 Quat q = load_quat(s.rot);
+                const bool qid = is_identity(q);
                 V3 sz = load3(s.shape);
                 if (KIND == 1) {
                     Bpi en, ex;
-                    int k = box_coef(sz, mo, md, en, ex);
-                    const double pb = prob_box(sz);
+                    int k = box_coef(sz, mo, md, same ? rc : make_rcp3(md), en, ex);
+                    const double pb = s.aux[0];
                     if (k == 2) {
                         V3 ng = normalize(rotate(q, bpi_normal(en)));
                         impact += pb * (en.t * en.t / fabs(dot(d, ng)));
@@ -265,14 +271,15 @@ RT_D void bvh_all(const DevBvh& B, V3 o, V3 d, Stack& S, Cnt<ST>& C, double& imp
                     }
                 } else {
                     double t1, t2;
-                    int k = ell_coef(sz, mo, md, t1, t2);
+                    const Radii R = load_radii(s);
+                    int k = ell_coef(R, mo, md, t1, t2);
                     if (k == 2) {
-                        V3 ng = normalize(rotate(q, ell_normal(sz, mo, md, t1)));
+                        V3 ng = normalize(rotate_fast(q, qid, ell_normal(R, mo, md, t1)));
                         impact += prob_ell(sz, ng) * (t1 * t1 / fabs(dot(d, ng)));
                         C.lhit(); nhits++;
                     }
                     if (k >= 1) {
-                        V3 ng = normalize(rotate(q, -ell_normal(sz, mo, md, t2)));
+                        V3 ng = normalize(rotate_fast(q, qid, -ell_normal(R, mo, md, t2)));
                         impact += prob_ell(sz, ng) * (t2 * t2 / fabs(dot(d, ng)));
                         C.lhit(); nhits++;
                     }
@@ -283,8 +290,8 @@ RT_D void bvh_all(const DevBvh& B, V3 o, V3 d, Stack& S, Cnt<ST>& C, double& imp
         if (left >= 0) {
             double lt, rt2;
             C.aabb(2);
-            bool lh = aabb_hit(load3(n.lmin), load3(n.lmax), o, d, lt);
-            bool rh = aabb_hit(load3(n.rmin), load3(n.rmax), o, d, rt2);
+            bool lh = aabb_hit(load3(n.lmin), load3(n.lmax), o, d, rc, lt);
+            bool rh = aabb_hit(load3(n.rmin), load3(n.rmax), o, d, rc, rt2);
             if (lh) {
                 if (rh) S.push((uint32_t)n.right, 0.0);
                 node = (uint32_t)left;
@@ -302,9 +309,10 @@ RT_D void bvh_all(const DevBvh& B, V3 o, V3 d, Stack& S, Cnt<ST>& C, double& imp
 template <bool ST>
 RT_D double lights_impact(const DevScene& S, V3 o, V3 d, Stack& stk, Cnt<ST>& C, uint32_t& nhits) {
     double impact = 0.0;
-    bvh_all<1, ST>(S.lboxes, o, d, stk, C, impact, nhits);
-    bvh_all<2, ST>(S.lells, o, d, stk, C, impact, nhits);
-    bvh_all<3, ST>(S.ltris, o, d, stk, C, impact, nhits);
+    const Rcp3 rc = make_rcp3(d);  // dead (DCE'd) unless RT_FASTDIV
+    bvh_all<1, ST>(S.lboxes, o, d, rc, stk, C, impact, nhits);
+    bvh_all<2, ST>(S.lells, o, d, rc, stk, C, impact, nhits);
+    bvh_all<3, ST>(S.ltris, o, d, rc, stk, C, impact, nhits);
     return impact;
 }
 template <bool ST>
@@ -350,10 +358,12 @@ RT_D V3 light_sample(const DevScene& S, V3 pos, Rng& r, const Scales& sc) {  // 
     V3 world;
     if (index < nb) {
         const DevShape l = S.lboxes.shapes[index];
-        world = rotate(load_quat(l.rot), uniform_on_box(load3(l.shape), r, sc)) + load3(l.pos);
+        const Quat q = load_quat(l.rot);
+        world = rotate_fast(q, is_identity(q), uniform_on_box(load3(l.shape), r, sc)) + load3(l.pos);
     } else if (index < (uint64_t)nb + ne) {
         const DevShape l = S.lells.shapes[index - nb];
-        world = rotate(load_quat(l.rot), mul(uniform_on_sphere(r), load3(l.shape))) + load3(l.pos);
+        const Quat q = load_quat(l.rot);
+        world = rotate_fast(q, is_identity(q), mul(uniform_on_sphere(r), load3(l.shape))) + load3(l.pos);
     } else {
         const DevTri t = S.ltris.tris[index - nb - ne];
         double u = gen_range_incl(r, 0.0, sc.s01);
@@ -458,7 +468,7 @@ RT_D void wave_flush(const Cnt<ST>& C, unsigned long long* stats) {
 
 // ------------------------------------------------------------ kernels ----
 template <bool ST, bool HIT>
-__global__ __launch_bounds__(kBlock) void path_kernel(DevScene S, KParams P, double* __restrict__ out,
+__global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void path_kernel(DevScene S, KParams P, double* __restrict__ out,
                                                       int32_t* __restrict__ hit_ids,
                                                       unsigned long long* __restrict__ stats,
                                                       uint32_t* spill_n, double* spill_t) {

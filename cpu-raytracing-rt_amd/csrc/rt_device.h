@@ -126,6 +126,45 @@ struct Cnt {
     RT_D void path() { if (ON) c.paths++; }
 };
 
+// ------------------------------------------------------ exact division ----
+// x / y correctly rounded from a precomputed r = RN(1/y): q0 = x*r, then two
+// FMA-residual corrections (Markstein: once q is within 1 ulp, q + (x - q*y)*r
+// rounds to RN(x/y); the first correction makes q0 faithful, the second
+// rounds).  The residuals x - q*y are exact (FMA) as long as nothing
+// under/overflows, which the exponent guard ensures: both |x| and |y| in
+// [2^-450, 2^451).  Outside it (incl. 0, inf, NaN, subnormals) the plain IEEE
+// division runs.  5 f64 ops instead of the ~10-op v_div_scale/v_rcp/v_div_fmas/
+// v_div_fixup sequence.  Checked bit-for-bit against x / y on 1.2e8 adversarial
+// pairs (tools/fastdiv_check.c) and by every parity test.
+RT_D bool fd_ok(double v) {
+    return (((uint32_t)((uint64_t)__double_as_longlong(v) >> 52) & 0x7ffu) - 573u) < 901u;
+}
+RT_D double fdiv_r(double x, double y, double r, bool yok) {
+#ifndef RT_FASTDIV  // opt-in: measured slower than the hardware sequence in the megakernel
+    return x / y;
+#endif
+    if (yok && fd_ok(x)) {
+        const double q0 = x * r;
+        const double e0 = fma(-q0, y, x);
+        const double q1 = fma(e0, r, q0);
+        const double e1 = fma(-q1, y, x);
+        return fma(e1, r, q1);
+    }
+    return x / y;
+}
+constexpr double kInvPi = 1.0 / kPi;  // RN(1/pi), folded exactly at compile time
+RT_D double div_pi(double x) { return fdiv_r(x, kPi, kInvPi, true); }
+
+// per-axis reciprocals of a ray direction (shared by every slab test of a ray)
+struct Rcp3 {
+    V3 r;
+    uint32_t ok;  // bit i: axis i usable by fdiv_r
+};
+RT_D Rcp3 make_rcp3(V3 d) {
+    return Rcp3{v3(1.0 / d.x, 1.0 / d.y, 1.0 / d.z),
+                (fd_ok(d.x) ? 1u : 0u) | (fd_ok(d.y) ? 2u : 0u) | (fd_ok(d.z) ? 4u : 0u)};
+}
+
 // ------------------------------------------------------------ geometry ----
 // AABB::intersects (aabb.rs:51-108)
 RT_D double safe_min(double a, double b) {
@@ -138,7 +177,7 @@ RT_D double safe_max(double a, double b) {
     if (!isfinite(b)) return a;
     return rmax(a, b);
 }
-RT_D bool aabb_hit(V3 mn, V3 mx, V3 o, V3 d, double& t) {
+RT_D bool aabb_hit(V3 mn, V3 mx, V3 o, V3 d, const Rcp3& rc, double& t) {
     if ((d.x == 0.0 && (o.x < mn.x || mx.x < o.x)) || (d.y == 0.0 && (o.y < mn.y || mx.y < o.y)) ||
         (d.z == 0.0 && (o.z < mn.z || mx.z < o.z)))
         return false;
@@ -146,7 +185,11 @@ RT_D bool aabb_hit(V3 mn, V3 mx, V3 o, V3 d, double& t) {
         t = 0.0;  // inside (aabb.rs:58-60)
         return true;
     }
-    V3 tmin = div(mn - o, d), tmax = div(mx - o, d);
+    const bool okx = rc.ok & 1u, oky = rc.ok & 2u, okz = rc.ok & 4u;
+    V3 tmin = v3(fdiv_r(mn.x - o.x, d.x, rc.r.x, okx), fdiv_r(mn.y - o.y, d.y, rc.r.y, oky),
+                 fdiv_r(mn.z - o.z, d.z, rc.r.z, okz));
+    V3 tmax = v3(fdiv_r(mx.x - o.x, d.x, rc.r.x, okx), fdiv_r(mx.y - o.y, d.y, rc.r.y, oky),
+                 fdiv_r(mx.z - o.z, d.z, rc.r.z, okz));
     double t1x = safe_min(tmin.x, tmax.x), t1y = safe_min(tmin.y, tmax.y), t1z = safe_min(tmin.z, tmax.z);
     double t2x = safe_max(tmin.x, tmax.x), t2y = safe_max(tmin.y, tmax.y), t2z = safe_max(tmin.z, tmax.z);
     double tn = safe_max(safe_max(t1x, t1y), t1z);
@@ -157,11 +200,35 @@ RT_D bool aabb_hit(V3 mn, V3 mx, V3 o, V3 d, double& t) {
     return false;
 }
 
-// model_space_ray (intersections.rs:93-99)
-RT_D void model_ray(const DevShape& s, V3 o, V3 d, V3& mo, V3& md) {
+// Quaternion::rotate_vector with an identity quaternion (s == 1, v == ±0):
+// every cross product term is a signed zero, so each NONZERO finite component
+// comes back bit-for-bit unchanged (x + ±0 == x).  Only a zero component can
+// change (its sign depends on the others), so vectors with a zero or
+// non-finite component take the generic formula.  Bit-exact either way.
+RT_D bool is_identity(const Quat& q) {
+#ifdef RT_NO_FASTROT  // ablation build
+    return false;
+#endif
+    return q.s == 1.0 && q.v.x == 0.0 && q.v.y == 0.0 && q.v.z == 0.0;
+}
+RT_D bool all_nonzero_finite(V3 v) {
+    return v.x != 0.0 && v.y != 0.0 && v.z != 0.0 && isfinite(v.x) && isfinite(v.y) && isfinite(v.z);
+}
+RT_D V3 rotate_fast(const Quat& q, bool ident, V3 v) {
+    if (ident && all_nonzero_finite(v)) return v;
+    return rotate(q, v);
+}
+
+// model_space_ray (intersections.rs:93-99).  Returns true when md == d bit for
+// bit (identity rotation, d without zero components): the caller may then
+// reuse the world ray's direction reciprocals.
+RT_D bool model_ray(const DevShape& s, V3 o, V3 d, V3& mo, V3& md) {
     Quat r = conjugate(load_quat(s.rot));
-    mo = rotate(r, o - load3(s.pos));
-    md = rotate(r, d);
+    const bool ident = is_identity(r);
+    mo = rotate_fast(r, ident, o - load3(s.pos));
+    const bool same = ident && all_nonzero_finite(d);
+    md = same ? d : rotate(r, d);
+    return same;
 }
 
 // Plane::intersection (plane.rs:11-21); aux bit0 = (nd <= 0)
@@ -176,14 +243,16 @@ RT_D bool plane_t(V3 n, V3 o, V3 d, double& t, uint32_t& aux) {
 
 // intersect_box_coef (box.rs:75-115). Entry/exit as (t, sign, dim).
 struct Bpi { double t; double sign; int dim; };
-RT_D int box_coef(V3 s, V3 o, V3 d, Bpi& en, Bpi& ex) {
+RT_D int box_coef(V3 s, V3 o, V3 d, const Rcp3& rc, Bpi& en, Bpi& ex) {
     bool have = false;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         double di = comp(d, i), oi = comp(o, i), si = comp(s, i);
         if (di == 0.0 && si < fabs(oi)) return 0;
         if (di == 0.0) continue;
-        double t1 = (si - oi) / di, t2 = (-si - oi) / di;
+        const double ri = comp(rc.r, i);
+        const bool ok = (rc.ok >> i) & 1u;
+        double t1 = fdiv_r(si - oi, di, ri, ok), t2 = fdiv_r(-si - oi, di, ri, ok);
         double a, b, nrm;
         if (t1 < t2) { a = t1; b = t2; nrm = 1.0; } else { a = t2; b = t1; nrm = -1.0; }
         if (!have) { en = Bpi{a, nrm, i}; ex = Bpi{b, nrm, i}; have = true; }
@@ -215,23 +284,39 @@ RT_D V3 aux_box_normal(uint32_t aux) {
     return v3(0.0, 0.0, s);
 }
 
+// Ellipsoid radii with their host-precomputed reciprocals (DevShape::aux).
+struct Radii {
+    V3 r, inv;
+    uint32_t ok;
+};
+RT_D Radii load_radii(const DevShape& s) {
+    V3 r = load3(s.shape);
+    return Radii{r, load3(s.aux), (fd_ok(r.x) ? 1u : 0u) | (fd_ok(r.y) ? 2u : 0u) | (fd_ok(r.z) ? 4u : 0u)};
+}
+RT_D V3 div_radii(V3 v, const Radii& R) {  // v.div_element_wise(r)
+    return v3(fdiv_r(v.x, R.r.x, R.inv.x, R.ok & 1u), fdiv_r(v.y, R.r.y, R.inv.y, R.ok & 2u),
+              fdiv_r(v.z, R.r.z, R.inv.z, R.ok & 4u));
+}
+
 // intersect_ellipsoid_coef (ellipsoid.rs:49-76)
-RT_D int ell_coef(V3 r, V3 o, V3 d, double& t1o, double& t2o) {
-    V3 oo = div(o, r), dd = div(d, r);
+RT_D int ell_coef(const Radii& R, V3 o, V3 d, double& t1o, double& t2o) {
+    V3 oo = div_radii(o, R), dd = div_radii(d, R);
     double c = dot(oo, oo), b = dot(oo, dd), a = dot(dd, dd);
     double disc = b * b - a * (c - 1.0);
     if (disc < 0.0) return 0;
     double ds = sqrt(disc);
-    double t1 = (-b + ds) / a, t2 = (-b - ds) / a;
+    const double ra = 1.0 / a;
+    const bool aok = fd_ok(a);
+    double t1 = fdiv_r(-b + ds, a, ra, aok), t2 = fdiv_r(-b - ds, a, ra, aok);
     if (t2 < t1) { double tmp = t1; t1 = t2; t2 = tmp; }
     t1o = t1; t2o = t2;
     if (0.0 <= t1) return 2;
     if (0.0 <= t2) return 1;
     return 0;
 }
-RT_D V3 ell_normal(V3 r, V3 o, V3 d, double t) {  // ellipsoid.rs:26,29
+RT_D V3 ell_normal(const Radii& R, V3 o, V3 d, double t) {  // ellipsoid.rs:26,29
     V3 p = o + d * t;
-    return normalize(div(div(p, r), r));
+    return normalize(div_radii(div_radii(p, R), R));
 }
 
 // Triangle::intersection (triangle.rs:49-80) up to (u, v, t); normals later.
@@ -240,7 +325,10 @@ RT_D bool tri_uvt(const DevTri& tr, V3 o, V3 d, double& u, double& v, double& t)
     double det = m0.x * (m1.y * m2.z - m2.y * m1.z) - m1.x * (m0.y * m2.z - m2.y * m0.z) +
                  m2.x * (m0.y * m1.z - m1.y * m0.z);
     if (fabs(det) < 1e-11) return false;
-    V3 x0 = cross(m1, m2) / det, x1 = cross(m2, m0) / det, x2 = cross(m0, m1) / det;
+    const double rd = 1.0 / det;
+    const bool ok = fd_ok(det);
+    auto dv = [&](V3 c) { return v3(fdiv_r(c.x, det, rd, ok), fdiv_r(c.y, det, rd, ok), fdiv_r(c.z, det, rd, ok)); };
+    V3 x0 = dv(cross(m1, m2)), x1 = dv(cross(m2, m0)), x2 = dv(cross(m0, m1));
     V3 w = o - load3(tr.a);
     double uu = dot(x0, w), vv = dot(x1, w), tt = dot(x2, w);
     if (uu < 0.0 || vv < 0.0 || 1.0 < uu + vv || tt < 0.0) return false;
@@ -252,7 +340,8 @@ RT_D bool tri_uvt(const DevTri& tr, V3 o, V3 d, double& u, double& v, double& t)
 struct Hit { double t; V3 ng, ns; bool inside; };
 
 RT_D Hit rotated(const Hit& h, Quat q) {  // with_rotated_normal (intersections.rs:32-39)
-    return Hit{h.t, normalize(rotate(q, h.ng)), normalize(rotate(q, h.ns)), h.inside};
+    const bool ident = is_identity(q);
+    return Hit{h.t, normalize(rotate_fast(q, ident, h.ng)), normalize(rotate_fast(q, ident, h.ns)), h.inside};
 }
 
 }  // namespace rt

@@ -30,8 +30,13 @@ struct alignas(16) DevShape {  // Primitive<T> hot part (scene.rs:20-27)
     double shape[3];           // plane normal | box half sizes | ellipsoid radii
     double pos[3];
     double rot[4];             // (s, x, y, z)
+    // host-precomputed constants (same IEEE ops as the device would do):
+    //   ellipsoid: aux = RN(1/r) per axis (exact reciprocal division, RT_FASTDIV)
+    //   box:       aux[0] = 1/sum/8 (intersection_probability.rs:15-23)
+    double aux[3];
+    double pad;
 };
-static_assert(sizeof(DevShape) == 80, "shape record");
+static_assert(sizeof(DevShape) == 112, "shape record");
 
 struct alignas(16) DevTri {    // Triangle hot part (triangle.rs:5-17)
     double a[3], ba[3], ca[3];

@@ -226,9 +226,16 @@ std::string build_scene(const rt_scene_desc& d, HostScene& out) {
         const rt_shape& s = d.shapes[i];
         if (s.material >= d.n_materials) return "shape material out of range";
         ShapeItem it;
+        std::memset(&it.s, 0, sizeof(it.s));
         std::memcpy(it.s.shape, s.shape, sizeof(it.s.shape));
         std::memcpy(it.s.pos, s.position, sizeof(it.s.pos));
         std::memcpy(it.s.rot, s.rotation, sizeof(it.s.rot));
+        if (s.type == RT_SHAPE_ELLIPSOID)
+            for (int k = 0; k < 3; ++k) it.s.aux[k] = 1.0 / s.shape[k];
+        if (s.type == RT_SHAPE_BOX) {
+            const double* z = s.shape;
+            it.s.aux[0] = 1.0 / ((z[1] * z[2] + z[0] * z[2]) + z[0] * z[1]) / 8.0;
+        }
         it.mat = s.material;
         it.gid = (int32_t)i;
         if (s.type == RT_SHAPE_PLANE) {  // Primitive::new_without_aabb (scene.rs:126-136)
