@@ -38,10 +38,30 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md "Chip-level para
 B_AABB, B_TRI, B_SHAPE, B_SHADE = 32, 72, 80, 100
 
 WORKLOADS = {
-    # name: (scene file, width, height, spp, depth override or None)
+    # name: (scene, width, height, spp, depth override or None); "gltf:<name>" = scenes/gen/<name>.gltf
     "C2": ("cornell.txt", 1920, 1080, 256, None),
     "C1": ("cornell.txt", 256, 256, 64, None),
+    "C3": ("gltf:sponza_like", 1920, 1080, 256, None),   # ray_depth 8 comes from the glTF builder
 }
+DESCRIPTIONS = {
+    "cornell.txt": "Cornell box (scenes/cornell.txt, custom format, 9 primitives, 1 emissive box light)",
+    "gltf:sponza_like": "synthetic Sponza-class atrium (scenes/gen_sponza_like.py -> glTF, 263k smooth-normal "
+                        "triangles, full BVH, emissive ceiling quad, black background)",
+}
+
+
+def load_workload(rt, scene_file, W, H, spp):
+    if scene_file.startswith("gltf:"):
+        name = scene_file[5:]
+        path = os.path.join(HERE, "scenes", "gen", name + ".gltf")
+        if not os.path.exists(path):  # deterministic generator; the asset is not committed
+            import subprocess
+            subprocess.run([sys.executable, os.path.join(HERE, "scenes", "gen_sponza_like.py"),
+                            os.path.join(HERE, "scenes", "gen"), "--name", name], check=True,
+                           stdout=subprocess.DEVNULL)
+        return rt.load_gltf(path, W, H, spp)
+    desc, params = rt.parse_scene(open(os.path.join(HERE, "scenes", scene_file)).read())
+    return desc, params.replace(width=W, height=H, spp=spp)
 
 
 def algo_bytes(st):
@@ -100,8 +120,9 @@ def main():
     scene_file, W, H, spp, depth = WORKLOADS[args.workload]
     if args.spp:
         spp = args.spp
-    desc, params = rt.parse_scene(open(os.path.join(HERE, "scenes", scene_file)).read())
-    params = params.replace(width=W, height=H, spp=spp, **({"ray_depth": depth} if depth else {}))
+    desc, params = load_workload(rt, scene_file, W, H, spp)
+    if depth:
+        params = params.replace(ray_depth=depth)
     t0 = time.perf_counter()
     scene = rt.Scene(desc)
     build_s = time.perf_counter() - t0
@@ -171,8 +192,9 @@ def main():
             "dtype": "f64",
             "data": "synthetic",
             "config": {
-                "workload": f"{args.workload}: Cornell box (scenes/{scene_file}, custom format, 9 primitives, "
-                            f"1 emissive box light), {W}x{H}, {spp} spp, ray_depth {params.ray_depth}",
+                "workload": f"{args.workload}: {DESCRIPTIONS[scene_file]}, {W}x{H}, {spp} spp, "
+                            f"ray_depth {params.ray_depth}",
+                "triangles": int(len(desc.tri_material)), "shapes": int(len(desc.shapes)),
                 "width": W, "height": H, "spp": spp, "ray_depth": params.ray_depth,
                 "paths_per_step": frame_paths, "segments_per_step": frame_segments,
                 "parallelism": f"tiles16x16 round-robin over {world} GPU(s) + 1 RCCL gather",

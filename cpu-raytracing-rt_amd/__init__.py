@@ -44,6 +44,8 @@ RT_FLAG_STATS, RT_FLAG_HIT_IDS = 0x1, 0x2
 RT_HIT_MISS, RT_HIT_NONE = -1, -2
 RT_TILE = 16
 ERRORS = {0: "OK", -1: "INVALID", -2: "DEVICE", -3: "NOMEM", -4: "PARSE", -5: "IO", -6: "UNSUPPORTED"}
+(RT_OK, RT_ERR_INVALID, RT_ERR_DEVICE, RT_ERR_NOMEM, RT_ERR_PARSE, RT_ERR_IO,
+ RT_ERR_UNSUPPORTED) = 0, -1, -2, -3, -4, -5, -6
 
 
 class rt_material(C.Structure):

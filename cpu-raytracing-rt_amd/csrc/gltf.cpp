@@ -390,6 +390,27 @@ bool load(Ctx& c, const std::string& path, uint32_t W, uint32_t H, uint32_t spp)
     if (const Json* tex = get_array(root, "textures", c.e, ok)) {
         for (const Json& t : tex->arr) { uint64_t s; if (!get_uint(t, "source", true, 0, s, c.e)) return false; }
     } else if (!ok) return false;
+    // serde deserialises every material and mesh up front, referenced or not (parser.rs:80-111)
+    if (const Json* ms = get_array(root, "materials", c.e, ok)) {
+        for (const Json& m : ms->arr) { rt_material tmp; if (!make_material(c, &m, tmp)) return false; }
+    } else if (!ok) return false;
+    if (const Json* ms = get_array(root, "meshes", c.e, ok)) {
+        for (const Json& m : ms->arr) {
+            const Json* prims = m.get("primitives");
+            if (!prims || prims->kind != Json::Array) return c.e.set(RT_ERR_PARSE, "missing field `primitives`");
+            for (const Json& p : prims->arr) {
+                const Json* attr = p.get("attributes");
+                uint64_t pos;
+                if (!attr) return c.e.set(RT_ERR_PARSE, "missing field `attributes`");
+                if (!get_uint(*attr, "POSITION", true, 0, pos, c.e)) return false;
+                bool has;
+                uint64_t v;
+                if (!get_opt_uint(*attr, "NORMAL", has, v, c.e) || !get_opt_uint(p, "indices", has, v, c.e) ||
+                    !get_opt_uint(p, "material", has, v, c.e) || !get_opt_uint(p, "mode", has, v, c.e))
+                    return false;
+            }
+        }
+    } else if (!ok) return false;
     // buffers / views / accessors
     const std::string prefix = path.substr(0, path.rfind('/') == std::string::npos ? 0 : path.rfind('/') + 1);
     if (const Json* bufs = get_array(root, "buffers", c.e, ok)) {
