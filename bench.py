@@ -42,6 +42,7 @@ WORKLOADS = {
     "C2": ("cornell.txt", 1920, 1080, 256, None),
     "C1": ("cornell.txt", 256, 256, 64, None),
     "C3": ("gltf:sponza_like", 1920, 1080, 256, None),   # ray_depth 8 comes from the glTF builder
+    "C4": ("gltf:sponza_like", 3840, 2160, 1024, None),  # BASELINE configs[3]: the 8-GPU scaling frame
 }
 DESCRIPTIONS = {
     "cornell.txt": "Cornell box (scenes/cornell.txt, custom format, 9 primitives, 1 emissive box light)",
@@ -66,6 +67,49 @@ def load_workload(rt, scene_file, W, H, spp):
 
 def algo_bytes(st):
     return B_AABB * st["aabb_tests"] + B_TRI * st["tri_tests"] + B_SHAPE * st["shape_tests"] + B_SHADE * st["shaded_hits"]
+
+
+PATH_KERNEL = "path_kernel<false, false>"
+
+
+def pmc_traffic(args):
+    """HBM bytes per launch of the timed path kernel, from two child rocprofv3
+    --pmc passes (FETCH_SIZE, then WRITE_SIZE: they do not fit one TCC pass) of
+    this same workload, run BEFORE this process initialises the GPU.  Correction
+    per MI355X_MICROARCH.md "HBM": FETCH_SIZE is in KiB and reports half the
+    bytes of 16-B/lane loads on gfx950 (the node/triangle loads are dwordx4),
+    so fetch bytes = 2 * 1024 * FETCH_SIZE; WRITE_SIZE is taken as reported."""
+    import csv
+    import shutil
+    import subprocess
+    import tempfile
+    if shutil.which("rocprofv3") is None:
+        return None, "rocprofv3 not found"
+    vals = {}
+    with tempfile.TemporaryDirectory(prefix="rt_pmc_") as td:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(td, counter)
+            cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "run", "--",
+                   sys.executable, os.path.abspath(__file__), "--workload", args.workload, "--steps", "1",
+                   "--warmup", "0", "--no-cpu-baseline", "--no-pmc"] + (["--spp", str(args.spp)] if args.spp else [])
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+            if r.returncode != 0:
+                return None, f"rocprofv3 --pmc {counter} failed rc={r.returncode}: {r.stderr[-300:]}"
+            rows = []
+            for root, _, files in os.walk(d):
+                for f in files:
+                    if f.endswith("counter_collection.csv"):
+                        rows += [x for x in csv.DictReader(open(os.path.join(root, f)))
+                                 if PATH_KERNEL in x["Kernel_Name"] and x["Counter_Name"] == counter]
+            if not rows:
+                return None, f"no {counter} rows for {PATH_KERNEL}"
+            vals[counter] = float(rows[-1]["Counter_Value"])
+    fetch = 2.0 * 1024.0 * vals["FETCH_SIZE"]
+    write = 1024.0 * vals["WRITE_SIZE"]
+    return fetch + write, {"FETCH_SIZE_KiB": vals["FETCH_SIZE"], "WRITE_SIZE_KiB": vals["WRITE_SIZE"],
+                           "fetch_bytes": fetch, "write_bytes": write,
+                           "correction": "fetch = 2 x 1024 x FETCH_SIZE (gfx950 16-B/lane loads); "
+                                         "write = 1024 x WRITE_SIZE", "kernel": PATH_KERNEL}
 
 
 def cpu_baseline(desc, params, target_s):
@@ -106,11 +150,15 @@ def main():
     ap.add_argument("--spp", type=int, default=None, help="override spp (not the headline config)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc child passes (traffic=null)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    traffic, traffic_detail = None, "not collected (N>1 or --no-pmc)"
+    if world == 1 and not args.no_pmc:  # before this process touches the GPU
+        traffic, traffic_detail = pmc_traffic(args)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -206,7 +254,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_detail": traffic_detail,
                 "kernel": "rt::path_kernel<false,false>",
                 "kernel_ms": kern_ms,
                 "algorithmic_bytes_per_launch": algo_bytes(st),

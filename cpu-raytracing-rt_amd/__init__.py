@@ -78,7 +78,7 @@ class rt_stats(C.Structure):
     _fields_ = [("paths", C.c_uint64), ("segments", C.c_uint64), ("aabb_tests", C.c_uint64),
                 ("tri_tests", C.c_uint64), ("shape_tests", C.c_uint64), ("shaded_hits", C.c_uint64),
                 ("light_queries", C.c_uint64), ("light_hits", C.c_uint64), ("kernel_ms", C.c_double),
-                ("total_ms", C.c_double)]
+                ("total_ms", C.c_double), ("lane_steps", C.c_uint64), ("wave_steps", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -108,6 +108,7 @@ EXPORTS = {
     "rt_scene_get_info": (C.c_int, [C.c_void_p, C.POINTER(rt_scene_info)]),
     "rt_render": (C.c_int, [C.c_void_p, C.POINTER(rt_render_params), C.c_void_p, C.c_void_p, C.POINTER(rt_stats)]),
     "rt_tiles_per_rank": (C.c_int, [C.POINTER(rt_render_params), C.c_uint32, C.POINTER(C.c_uint32)]),
+    "rt_sample_chunks": (C.c_int, [C.POINTER(rt_render_params), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     "rt_render_tiles_async": (C.c_int, [C.c_void_p, C.POINTER(rt_render_params), C.c_uint32, C.c_uint32,
                                         C.c_void_p, C.c_void_p]),
     "rt_read_stats": (C.c_int, [C.c_void_p, C.POINTER(rt_stats), C.c_int]),
@@ -467,6 +468,13 @@ def build_bvh(boxes: np.ndarray):
                               links.ctypes.data_as(C.c_void_p), bounds.ctypes.data_as(C.c_void_p),
                               order.ctypes.data_as(C.c_void_p), C.byref(depth)))
     return links, bounds, order, depth.value
+
+
+def sample_chunks(params: RenderParams):
+    """(chunks, chunk_spp) of the device's work units for this frame (rt_sample_chunks)."""
+    k, cs = C.c_uint32(), C.c_uint32()
+    _check(lib().rt_sample_chunks(C.byref(params.to_c()), C.byref(k), C.byref(cs)))
+    return k.value, cs.value
 
 
 def probe_fp64(op: int, a: np.ndarray, b: Optional[np.ndarray] = None) -> np.ndarray:

@@ -4,8 +4,10 @@
 // (the reference panics).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -46,6 +48,13 @@ struct rt_scene {
     uint32_t* spill_n = nullptr;
     double* spill_t = nullptr;
     size_t spill_entries = 0;
+    // chunk partial sums (KParams::chunks > 1), grown on demand
+    double* part = nullptr;
+    size_t part_entries = 0;
+    // persistent path kernel: wave-tile queue and per-wave sample ring
+    uint32_t* queue = nullptr;
+    double* ring = nullptr;
+    size_t ring_entries = 0;
     unsigned long long* d_stats = nullptr;
 };
 
@@ -89,6 +98,9 @@ void free_scene(rt_scene* s) {
     for (void* p : s->allocs) (void)hipFree(p);
     if (s->spill_n) (void)hipFree(s->spill_n);
     if (s->spill_t) (void)hipFree(s->spill_t);
+    if (s->part) (void)hipFree(s->part);
+    if (s->queue) (void)hipFree(s->queue);
+    if (s->ring) (void)hipFree(s->ring);
     if (s->d_stats) (void)hipFree(s->d_stats);
     (void)hipSetDevice(cur);
     delete s;
@@ -101,6 +113,20 @@ int check_params(const rt_render_params* p) {
     if (p->ray_depth > 255) return set_error(RT_ERR_INVALID, "ray_depth is a u8 in the reference (scene.rs:85)");
     if (p->fov_axis != RT_FOV_X && p->fov_axis != RT_FOV_Y) return set_error(RT_ERR_INVALID, "bad fov_axis");
     return RT_OK;
+}
+
+// Sample chunking of a frame (render.h sample_chunks).  RT_CHUNK_SPP=<n>
+// overrides the run length for tuning experiments only; rt_sample_chunks
+// reports the override too, so checkers stay consistent.
+void frame_chunks(const rt_render_params* p, uint32_t& chunks, uint32_t& chunk_spp) {
+    sample_chunks(p->width, p->height, p->spp, chunks, chunk_spp);
+    if (const char* e = std::getenv("RT_CHUNK_SPP")) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v > 0) {
+            chunk_spp = (uint32_t)std::min<long>(v, p->spp);
+            chunks = (p->spp + chunk_spp - 1) / chunk_spp;
+        }
+    }
 }
 
 // Camera::new (camera.rs:17-46) on the host + the tile map of one rank.
@@ -130,10 +156,23 @@ KParams make_kparams(const rt_render_params* p, uint32_t rank, uint32_t world) {
     k.tiles_x = (p->width + RT_TILE - 1) / RT_TILE;
     k.tiles_y = (p->height + RT_TILE - 1) / RT_TILE;
     k.n_tiles = (uint64_t)k.tiles_x * k.tiles_y;
+    k.n_slots = (uint32_t)((k.n_tiles + world - 1) / world);
+    frame_chunks(p, k.chunks, k.chunk_spp);
     return k;
 }
 
-uint32_t slots_per_rank(const KParams& k) { return (uint32_t)((k.n_tiles + k.world - 1) / k.world); }
+uint32_t slots_per_rank(const KParams& k) { return k.n_slots; }
+
+int ensure_part(rt_scene* s, const KParams& k) {
+    if (k.chunks == 1) return RT_OK;
+    const size_t need = (size_t)k.n_slots * k.chunks * 256 * 3;
+    if (need <= s->part_entries) return RT_OK;
+    if (s->part) (void)hipFree(s->part);
+    s->part = nullptr; s->part_entries = 0;
+    HIP_TRY(hipMalloc(&s->part, need * sizeof(double)));
+    s->part_entries = need;
+    return RT_OK;
+}
 
 // Spill area for stack entries beyond the LDS short stack: depth bound of the
 // deepest BVH, one slot per launched lane.
@@ -148,6 +187,38 @@ int ensure_spill(rt_scene* s, uint64_t lanes) {
     HIP_TRY(hipMalloc(&s->spill_n, need * sizeof(uint32_t)));
     HIP_TRY(hipMalloc(&s->spill_t, need * sizeof(double)));
     s->spill_entries = need;
+    return RT_OK;
+}
+
+// Workspace of one path-kernel launch: persistent grid size, then the spill,
+// ring and chunk-partial buffers sized for it (all grow-only, scene-owned).
+int prepare_path(rt_scene* s, const KParams& k, bool stats, bool hits, PathWork& W) {
+    const uint64_t n_units = (uint64_t)k.n_slots * k.chunks * 4;
+    if (n_units >= (1ull << 31)) return set_error(RT_ERR_INVALID, "frame too large for one launch");
+    std::memset(&W, 0, sizeof(W));
+    HIP_TRY(path_grid(stats, hits, (uint32_t)n_units, &W.grid));
+    int rc;
+    if ((rc = ensure_spill(s, (uint64_t)W.grid * 64)) || (rc = ensure_part(s, k))) return rc;
+    if (!s->queue) HIP_TRY(hipMalloc(&s->queue, sizeof(uint32_t)));
+    const size_t ring_need = (size_t)W.grid * kRingRows * 64 * 3;
+    if (ring_need > s->ring_entries) {
+        if (s->ring) (void)hipFree(s->ring);
+        s->ring = nullptr; s->ring_entries = 0;
+        HIP_TRY(hipMalloc(&s->ring, ring_need * sizeof(double)));
+        s->ring_entries = ring_need;
+    }
+    W.queue = s->queue; W.ring = s->ring; W.part = s->part;
+    W.spill_n = s->spill_n; W.spill_t = s->spill_t;
+    return RT_OK;
+}
+
+// device counters (render.hip wave_flush order) -> rt_stats (timings untouched)
+int copy_stats(rt_scene* s, rt_stats* out) {
+    unsigned long long c[kNStats];
+    HIP_TRY(hipMemcpy(c, s->d_stats, sizeof(c), hipMemcpyDeviceToHost));
+    out->paths = c[0]; out->segments = c[1]; out->aabb_tests = c[2]; out->tri_tests = c[3];
+    out->shape_tests = c[4]; out->shaded_hits = c[5]; out->light_queries = c[6]; out->light_hits = c[7];
+    out->lane_steps = c[8]; out->wave_steps = c[9];
     return RT_OK;
 }
 
@@ -201,8 +272,8 @@ int rt_scene_create(const rt_scene_desc* desc, rt_scene** out) {
         s->info.bvh_nodes[k] = hs.bvh[k].nodes.size();
         s->info.bvh_depth[k] = hs.bvh[k].depth;
     }
-    HIP_TRY(hipMalloc(&s->d_stats, 8 * sizeof(unsigned long long)));
-    HIP_TRY(hipMemset(s->d_stats, 0, 8 * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&s->d_stats, kNStats * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(s->d_stats, 0, kNStats * sizeof(unsigned long long)));
     s->info.n_planes = d.n_planes;
     s->info.n_boxes = d.boxes.n_prims;
     s->info.n_ellipsoids = d.ells.n_prims;
@@ -232,6 +303,14 @@ int rt_tiles_per_rank(const rt_render_params* p, uint32_t world, uint32_t* n) {
     return RT_OK;
 }
 
+int rt_sample_chunks(const rt_render_params* p, uint32_t* chunks, uint32_t* chunk_spp) {
+    int rc = check_params(p);
+    if (rc) return rc;
+    if (!chunks || !chunk_spp) return set_error(RT_ERR_INVALID, "output is NULL");
+    frame_chunks(p, *chunks, *chunk_spp);
+    return RT_OK;
+}
+
 int rt_render_tiles_async(rt_scene* s, const rt_render_params* p, uint32_t rank, uint32_t world,
                           double* d_tile_rgb, void* stream) {
     int rc = check_params(p);
@@ -239,10 +318,10 @@ int rt_render_tiles_async(rt_scene* s, const rt_render_params* p, uint32_t rank,
     if (!s || !d_tile_rgb) return set_error(RT_ERR_INVALID, "scene/output is NULL");
     if (world == 0 || rank >= world) return set_error(RT_ERR_INVALID, "rank must be < world");
     KParams k = make_kparams(p, rank, world);
-    uint32_t slots = slots_per_rank(k);
-    if ((rc = ensure_spill(s, (uint64_t)slots * 256))) return rc;
-    HIP_TRY(launch_path(s->dev, k, slots, d_tile_rgb, nullptr, (p->flags & RT_FLAG_STATS) ? s->d_stats : nullptr,
-                        s->spill_n, s->spill_t, (hipStream_t)stream));
+    const bool want_stats = (p->flags & RT_FLAG_STATS) != 0;
+    PathWork W;
+    if ((rc = prepare_path(s, k, want_stats, false, W))) return rc;
+    HIP_TRY(launch_path(s->dev, k, W, d_tile_rgb, nullptr, want_stats ? s->d_stats : nullptr, (hipStream_t)stream));
     return RT_OK;
 }
 
@@ -250,12 +329,10 @@ int rt_read_stats(rt_scene* s, rt_stats* out, int reset) {
     if (!s || !out) return set_error(RT_ERR_INVALID, "scene/out is NULL");
     HIP_TRY(hipSetDevice(s->device));
     HIP_TRY(hipDeviceSynchronize());
-    unsigned long long c[8];
-    HIP_TRY(hipMemcpy(c, s->d_stats, sizeof(c), hipMemcpyDeviceToHost));
     std::memset(out, 0, sizeof(*out));
-    out->paths = c[0]; out->segments = c[1]; out->aabb_tests = c[2]; out->tri_tests = c[3];
-    out->shape_tests = c[4]; out->shaded_hits = c[5]; out->light_queries = c[6]; out->light_hits = c[7];
-    if (reset) HIP_TRY(hipMemset(s->d_stats, 0, sizeof(c)));
+    int rc = copy_stats(s, out);
+    if (rc) return rc;
+    if (reset) HIP_TRY(hipMemset(s->d_stats, 0, kNStats * sizeof(unsigned long long)));
     return RT_OK;
 }
 
@@ -282,20 +359,21 @@ int rt_render(rt_scene* s, const rt_render_params* p, double* out_mean_rgb, int3
     const uint64_t npx = (uint64_t)p->width * p->height;
     const bool want_hits = opt_hit_ids && (p->flags & RT_FLAG_HIT_IDS);
     const bool want_stats = opt_stats && (p->flags & RT_FLAG_STATS);
-    if ((rc = ensure_spill(s, (uint64_t)slots * 256))) return rc;
+    PathWork W;
+    if ((rc = prepare_path(s, k, want_stats, want_hits, W))) return rc;
     DevBuf<double> tiles, img;
     DevBuf<int32_t> hits;
     HIP_TRY(tiles.alloc((size_t)slots * 256 * 3));
     HIP_TRY(img.alloc(npx * 3));
     const uint64_t nhits = npx * p->spp * p->ray_depth;
     if (want_hits) HIP_TRY(hits.alloc(nhits));
-    if (want_stats) HIP_TRY(hipMemset(s->d_stats, 0, 8 * sizeof(unsigned long long)));
+    if (want_stats) HIP_TRY(hipMemset(s->d_stats, 0, kNStats * sizeof(unsigned long long)));
     hipEvent_t e0, e1;
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));
     HIP_TRY(hipEventRecord(e0, 0));
-    hipError_t le = launch_path(s->dev, k, slots, tiles.p, want_hits ? hits.p : nullptr,
-                                want_stats ? s->d_stats : nullptr, s->spill_n, s->spill_t, 0);
+    hipError_t le = launch_path(s->dev, k, W, tiles.p, want_hits ? hits.p : nullptr,
+                                want_stats ? s->d_stats : nullptr, 0);
     HIP_TRY(hipEventRecord(e1, 0));
     if (le != hipSuccess) {
         (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
@@ -311,13 +389,7 @@ int rt_render(rt_scene* s, const rt_render_params* p, double* out_mean_rgb, int3
     if (want_hits) HIP_TRY(hipMemcpy(opt_hit_ids, hits.p, nhits * sizeof(int32_t), hipMemcpyDeviceToHost));
     if (opt_stats) {
         std::memset(opt_stats, 0, sizeof(*opt_stats));
-        if (want_stats) {
-            unsigned long long c[8];
-            HIP_TRY(hipMemcpy(c, s->d_stats, sizeof(c), hipMemcpyDeviceToHost));
-            opt_stats->paths = c[0]; opt_stats->segments = c[1]; opt_stats->aabb_tests = c[2];
-            opt_stats->tri_tests = c[3]; opt_stats->shape_tests = c[4]; opt_stats->shaded_hits = c[5];
-            opt_stats->light_queries = c[6]; opt_stats->light_hits = c[7];
-        }
+        if (want_stats && (rc = copy_stats(s, opt_stats))) return rc;
         opt_stats->kernel_ms = ms;
         opt_stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }

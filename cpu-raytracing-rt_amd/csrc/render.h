@@ -22,10 +22,44 @@ struct KParams {
     uint32_t rank, world;
     uint32_t tiles_x, tiles_y;
     uint64_t n_tiles;
+    // sample chunking (DESIGN.md §4 "work units"): a work unit is (tile slot,
+    // chunk of chunk_spp consecutive samples); chunks == 1 writes means directly
+    uint32_t chunks, chunk_spp;
+    uint32_t n_slots, _pad;
 };
 
-hipError_t launch_path(const DevScene& S, const KParams& P, uint32_t n_slots, double* out, int32_t* hit_ids,
-                       unsigned long long* stats, uint32_t* spill_n, double* spill_t, hipStream_t st);
+// device work counters: paths, segments, aabb, tri, shape, shaded, light queries,
+// light hits, lane steps, wave steps (64 x longest lane) — rt_stats order
+constexpr int kNStats = 10;
+
+// Chunk count for a frame: a function of (W, H, spp) only, so the image does not
+// depend on the number of GPUs.  Doubles while the frame has < kChunkLanes
+// work units, capped at spp and kMaxChunks, then trimmed so no chunk is empty.
+constexpr uint64_t kChunkLanes = 16000000;
+constexpr uint32_t kMaxChunks = 64;
+inline void sample_chunks(uint32_t W, uint32_t H, uint32_t spp, uint32_t& chunks, uint32_t& chunk_spp) {
+    const uint64_t px = (uint64_t)W * H;
+    uint32_t k = 1;
+    while (k * 2 <= spp && k < kMaxChunks && px * k < kChunkLanes) k *= 2;
+    chunk_spp = (spp + k - 1) / k;
+    chunks = (spp + chunk_spp - 1) / chunk_spp;
+}
+
+// Device workspace of one path-kernel launch (owned by the scene).
+struct PathWork {
+    uint32_t grid;        // persistent waves (path_grid)
+    uint32_t* queue;      // wave-tile counter, zeroed by launch_path
+    double* ring;         // [grid][kRing=8][64][3] finished-path radiance
+    double* part;         // [n_slots*chunks][256][3] chunk partial sums (chunks > 1)
+    uint32_t* spill_n;    // traversal-stack spill, stride grid*64
+    double* spill_t;
+};
+constexpr uint32_t kRingRows = 8;   // render.hip kRing
+
+hipError_t path_grid(bool stats, bool hits, uint32_t n_units, uint32_t* grid);
+hipError_t launch_path(const DevScene& S, const KParams& P, const PathWork& W, double* out, int32_t* hit_ids,
+                       unsigned long long* stats, hipStream_t st);
+hipError_t launch_reduce_chunks(const double* part, double* out, const KParams& P, hipStream_t st);
 hipError_t launch_intersect(const DevScene& S, const double* rays, uint32_t n, rt_hit* out, uint32_t* spill_n,
                             double* spill_t, hipStream_t st);
 hipError_t launch_light(const DevScene& S, const double* rays, uint32_t n, int mode, double* out, uint32_t* cnt,

@@ -19,6 +19,8 @@
 // recursive "visit near, then far if still < best".
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "render.h"
 #include "rt_device.h"
 
@@ -31,24 +33,38 @@ constexpr int kBlock = 256;
 constexpr int kShort = kMaxBvhDepthShort;
 
 // ---------------------------------------------------------------- stack ---
+// LDS short stack laid out per wave: [wave][slot][lane], so consecutive lanes
+// hit consecutive banks for any block size.
+constexpr int kWave = 64;
 struct Stack {
-    uint32_t* sn;        // LDS node slots, stride kBlock
-    double* st;          // LDS entry-t slots, stride kBlock
+    uint32_t* sn;        // LDS node slots, stride kWave
+    double* st;          // LDS entry-t slots, stride kWave
     uint32_t* gn;        // global spill (stride = spill_stride) or null
     double* gt;
     uint32_t stride;
     int sp;
     RT_D void push(uint32_t node, double t) {
-        if (sp < kShort) { sn[sp * kBlock] = node; st[sp * kBlock] = t; }
+        if (sp < kShort) { sn[sp * kWave] = node; st[sp * kWave] = t; }
         else { gn[(size_t)(sp - kShort) * stride] = node; gt[(size_t)(sp - kShort) * stride] = t; }
         ++sp;
     }
     RT_D void pop(uint32_t& node, double& t) {
         --sp;
-        if (sp < kShort) { node = sn[sp * kBlock]; t = st[sp * kBlock]; }
+        if (sp < kShort) { node = sn[sp * kWave]; t = st[sp * kWave]; }
         else { node = gn[(size_t)(sp - kShort) * stride]; t = gt[(size_t)(sp - kShort) * stride]; }
     }
 };
+RT_D Stack make_stack(uint32_t* s_n, double* s_t, uint32_t tid, uint64_t gtid, uint32_t* spill_n, double* spill_t,
+                      uint32_t spill_stride) {
+    Stack k;
+    const uint32_t base = (tid / kWave) * kShort * kWave + tid % kWave;
+    k.sn = s_n + base; k.st = s_t + base;
+    k.gn = spill_n ? spill_n + gtid : nullptr;
+    k.gt = spill_t ? spill_t + gtid : nullptr;
+    k.stride = spill_stride;
+    k.sp = 0;
+    return k;
+}
 
 // Best candidate of one query: materialised into a Hit only for the winner.
 struct Cand {
@@ -454,7 +470,7 @@ RT_D bool segment(const DevScene& S, const KParams& P, const Scales& sc, PathSta
 }
 
 template <bool ST>
-RT_D void wave_flush(const Cnt<ST>& C, unsigned long long* stats) {
+RT_D void wave_flush(const Cnt<ST>& C, unsigned long long* stats, uint32_t wave_iters) {
     if (!ST) return;
     uint32_t v[8] = {C.c.paths, C.c.segments, C.c.aabb, C.c.tri, C.c.shape, C.c.shaded, C.c.lq, C.c.lhits};
 #pragma unroll
@@ -464,77 +480,144 @@ RT_D void wave_flush(const Cnt<ST>& C, unsigned long long* stats) {
         for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
         if ((threadIdx.x & 63) == 0 && x) atomicAdd(&stats[k], x);
     }
+    // lane utilisation: path steps summed over lanes vs 64 x the wave's loop iterations
+    unsigned long long s = C.c.steps;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if ((threadIdx.x & 63) == 0 && wave_iters) {
+        atomicAdd(&stats[8], s);
+        atomicAdd(&stats[9], 64ull * wave_iters);
+    }
 }
 
 // ------------------------------------------------------------ kernels ----
+// path_kernel — persistent waves (one 64-lane wave per workgroup, as many as
+// fit on the chip) pull wave-tiles from a global queue.  A wave-tile is
+// (tile slot, sample chunk, 8x8 quadrant): 64 pixels x chunk_spp samples.
+// Inside it the lanes take (sample row, pixel) paths dynamically in row-major
+// order — a lane whose path ends starts the next one at once, so lanes do not
+// idle while the wave's longest path finishes (rt_stats lane/wave steps).  A
+// finished path's radiance goes to a per-wave ring of kRing sample rows; a row
+// is committed once all 64 of its paths are done, each lane adding its OWN
+// pixel's value — so every pixel is still summed in sample order
+// (main.rs:94-104; bit-identical to the sequential sum when chunks == 1).
+constexpr int kRing = (int)kRingRows;
+
 template <bool ST, bool HIT>
-__global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void path_kernel(DevScene S, KParams P, double* __restrict__ out,
-                                                      int32_t* __restrict__ hit_ids,
-                                                      unsigned long long* __restrict__ stats,
-                                                      uint32_t* spill_n, double* spill_t) {
-    __shared__ uint32_t s_n[kShort * kBlock];
-    __shared__ double s_t[kShort * kBlock];
-    const uint32_t tid = threadIdx.x;
-    const uint64_t slot = blockIdx.x;
-    const uint64_t tile = (uint64_t)P.rank + slot * P.world;
-    const uint32_t wave = tid >> 6, lane = tid & 63;
-    const uint32_t lx = (wave & 1u) * 8u + (lane & 7u), ly = (wave >> 1) * 8u + (lane >> 3);
-    double* o = out + (slot * (uint64_t)kBlock + ly * RT_TILE + lx) * 3;
+__global__ __launch_bounds__(kWave, RT_MIN_WAVES) void path_kernel(DevScene S, KParams P, double* __restrict__ out,
+                                                     double* __restrict__ part, int32_t* __restrict__ hit_ids,
+                                                     unsigned long long* __restrict__ stats, uint32_t* spill_n,
+                                                     double* spill_t, uint32_t* __restrict__ queue,
+                                                     double* __restrict__ ring_all) {
+    __shared__ uint32_t s_n[kShort * kWave];
+    __shared__ double s_t[kShort * kWave];
+    __shared__ uint32_t s_cnt[kRing];  // finished paths per ring row
+    const uint32_t lane = threadIdx.x;
+    Stack stk = make_stack(s_n, s_t, lane, (uint64_t)blockIdx.x * kWave + lane, spill_n, spill_t,
+                           gridDim.x * kWave);
+    double* ring = ring_all + (uint64_t)blockIdx.x * kRing * kWave * 3;
+    const Scales sc{P.scale01, P.scale11};
+    const uint32_t depth = P.ray_depth;
+    const uint32_t n_units = P.n_slots * P.chunks * 4u;
+    const uint64_t below = (1ull << lane) - 1ull;
     Cnt<ST> C;
     C.zero();
-    V3 sum = v3(0.0, 0.0, 0.0);
-    const uint32_t px = (uint32_t)(tile % P.tiles_x) * RT_TILE + lx;
-    const uint32_t py = (uint32_t)(tile / P.tiles_x) * RT_TILE + ly;
-    if (tile < P.n_tiles && px < P.width && py < P.height) {
-        Stack stk;
-        stk.sn = s_n + tid; stk.st = s_t + tid;
-        const uint64_t gtid = (uint64_t)blockIdx.x * kBlock + tid;
-        stk.gn = spill_n ? spill_n + gtid : nullptr;
-        stk.gt = spill_t ? spill_t + gtid : nullptr;
-        stk.stride = (uint32_t)gridDim.x * kBlock;
-        stk.sp = 0;
-        const Scales sc{P.scale01, P.scale11};
-        const uint64_t pixel = (uint64_t)py * P.width + px;
-        const uint32_t spp = P.spp, depth = P.ray_depth;
+    for (;;) {  // wave-tiles; every wave leaves once the queue passes n_units
+        uint32_t u = 0;
+        if (lane == 0) u = atomicAdd(queue, 1u);
+        const uint32_t unit = __builtin_amdgcn_readfirstlane(u);
+        if (unit >= n_units) break;
+        const uint32_t quad = unit & 3u, sci = unit >> 2;  // sci = slot * chunks + chunk
+        const uint32_t slot = sci / P.chunks, chunk = sci % P.chunks;
+        const uint64_t tile = (uint64_t)P.rank + (uint64_t)slot * P.world;
+        const bool tile_ok = tile < P.n_tiles;
+        const uint32_t qx0 = (uint32_t)(tile % P.tiles_x) * RT_TILE + (quad & 1u) * 8u;
+        const uint32_t qy0 = (uint32_t)(tile / P.tiles_x) * RT_TILE + (quad >> 1) * 8u;
+        const uint32_t s0 = chunk * P.chunk_spp;
+        const uint32_t nrows = min(P.spp, s0 + P.chunk_spp) - s0, total = nrows * kWave;
+        if (lane < kRing) s_cnt[lane] = 0;
+        __syncthreads();
+        V3 sum = v3(0.0, 0.0, 0.0);
+        uint32_t base = 0, next = 0, witers = 0;  // wave-uniform schedule
+        bool busy = false;
+        uint32_t cur = 0, s = 0, b = 0;
+        uint64_t pixel = 0;
         PathState ps;
         Rng rng;
-        uint32_t s = 0, b = 0;
-        bool fresh = true;
         for (;;) {
-            if (fresh) {  // Camera::fuzzy_ray + raytrace (camera.rs:48-55, raytrace.rs:8-10)
-                if (s >= spp) break;
-                rng_init(rng, P.seed, pixel, s);
-                const double fx = (double)px + gen_range(rng, 0.0, 1.0);
-                const double fy = (double)py + gen_range(rng, 0.0, 1.0);
-                const double x = (2.0 * fx / P.fw - 1.0) * P.tan_x;
-                const double y = -(2.0 * fy / P.fh - 1.0) * P.tan_y;
-                const V3 dir = (load3(P.cam_right) * x + load3(P.cam_up) * y) + load3(P.cam_fwd) * 1.0;
-                ps.o = load3(P.cam_pos);
-                ps.d = normalize(dir);
-                ps.T = v3(1.0, 1.0, 1.0);
-                ps.L = v3(0.0, 0.0, 0.0);
-                b = 0;
-                fresh = false;
-                C.path();
+            // hand the next units to idle lanes, in lane order, inside the ring window
+            const uint32_t limit = min(total, (base + kRing) * kWave);
+            const uint64_t idle = __ballot(!busy);
+            if (next < limit && idle) {
+                const uint32_t k = (uint32_t)__popcll(idle & below);
+                if (!busy && next + k < limit) {
+                    cur = next + k;
+                    const uint32_t col = cur % kWave;
+                    const uint32_t px = qx0 + (col & 7u), py = qy0 + (col >> 3);
+                    s = s0 + cur / kWave;
+                    if (tile_ok && px < P.width && py < P.height) {
+                        // Camera::fuzzy_ray + raytrace (camera.rs:48-55, raytrace.rs:8-10)
+                        pixel = (uint64_t)py * P.width + px;
+                        rng_init(rng, P.seed, pixel, s);
+                        const double fx = (double)px + gen_range(rng, 0.0, 1.0);
+                        const double fy = (double)py + gen_range(rng, 0.0, 1.0);
+                        const double x = (2.0 * fx / P.fw - 1.0) * P.tan_x;
+                        const double y = -(2.0 * fy / P.fh - 1.0) * P.tan_y;
+                        const V3 dir = (load3(P.cam_right) * x + load3(P.cam_up) * y) + load3(P.cam_fwd) * 1.0;
+                        ps.o = load3(P.cam_pos);
+                        ps.d = normalize(dir);
+                        ps.T = v3(1.0, 1.0, 1.0);
+                        ps.L = v3(0.0, 0.0, 0.0);
+                        b = 0;
+                        busy = true;
+                        C.path();
+                    } else {
+                        atomicAdd(&s_cnt[(cur / kWave) % kRing], 1u);  // no pixel: done at once, never read
+                    }
+                }
+                next = min(limit, next + (uint32_t)__popcll(idle));
             }
-            bool cont = false;
-            if (b < depth) {
-                int32_t g;
-                cont = segment<ST>(S, P, sc, ps, rng, stk, C, g);
-                if (HIT) hit_ids[(pixel * spp + s) * depth + b] = g;
-                ++b;
+            // one segment of every live path
+            if (busy) {
+                C.step();
+                bool cont = false;
+                if (b < depth) {
+                    int32_t g;
+                    cont = segment<ST>(S, P, sc, ps, rng, stk, C, g);
+                    if (HIT) hit_ids[(pixel * P.spp + s) * depth + b] = g;
+                    ++b;
+                }
+                if (!cont || b >= depth) {
+                    if (HIT) for (uint32_t k = b; k < depth; ++k) hit_ids[(pixel * P.spp + s) * depth + k] = RT_HIT_NONE;
+                    const uint32_t r = (cur / kWave) % kRing;
+                    double* rp = ring + ((uint64_t)r * kWave + cur % kWave) * 3;
+                    rp[0] = ps.L.x; rp[1] = ps.L.y; rp[2] = ps.L.z;
+                    atomicAdd(&s_cnt[r], 1u);
+                    busy = false;
+                }
             }
-            if (!cont || b >= depth) {
-                if (HIT) for (uint32_t k = b; k < depth; ++k) hit_ids[(pixel * spp + s) * depth + k] = RT_HIT_NONE;
-                sum = sum + ps.L;
-                ++s;
-                fresh = true;
+            ++witers;
+            // commit complete rows in sample order (ring stores visible to the wave)
+            __syncthreads();
+            while (base < nrows && s_cnt[base % kRing] == (uint32_t)kWave) {
+                const double* rp = ring + ((uint64_t)(base % kRing) * kWave + lane) * 3;
+                sum = sum + v3(rp[0], rp[1], rp[2]);
+                __syncthreads();
+                if (lane == 0) s_cnt[base % kRing] = 0;
+                __syncthreads();
+                ++base;
             }
+            if (base >= nrows) break;
         }
-        sum = sum / (double)spp;  // main.rs:104 (mean, before tonemapping)
+        const uint32_t lx = (quad & 1u) * 8u + (lane & 7u), ly = (quad >> 1) * 8u + (lane >> 3);
+        const bool own = tile_ok && qx0 + (lane & 7u) < P.width && qy0 + (lane >> 3) < P.height;
+        V3 res = own ? (P.chunks == 1 ? sum / (double)P.spp : sum) : v3(0.0, 0.0, 0.0);  // main.rs:104
+        double* o = P.chunks == 1 ? out + ((uint64_t)slot * kBlock + ly * RT_TILE + lx) * 3
+                                  : part + ((uint64_t)sci * kBlock + ly * RT_TILE + lx) * 3;
+        o[0] = res.x; o[1] = res.y; o[2] = res.z;
+        wave_flush<ST>(C, stats, witers);
+        C.zero();
     }
-    o[0] = sum.x; o[1] = sum.y; o[2] = sum.z;
-    wave_flush<ST>(C, stats);
 }
 
 __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S, const double* __restrict__ rays, uint32_t n,
@@ -544,10 +627,7 @@ __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S, const dou
     __shared__ double s_t[kShort * kBlock];
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
-    Stack stk;
-    stk.sn = s_n + threadIdx.x; stk.st = s_t + threadIdx.x;
-    stk.gn = spill_n ? spill_n + i : nullptr; stk.gt = spill_t ? spill_t + i : nullptr;
-    stk.stride = gridDim.x * kBlock; stk.sp = 0;
+    Stack stk = make_stack(s_n, s_t, threadIdx.x, i, spill_n, spill_t, gridDim.x * kBlock);
     Cnt<false> C;
     Hit h; uint32_t mat; int32_t gid;
     V3 o = load3(rays + 6 * (size_t)i), d = load3(rays + 6 * (size_t)i + 3);
@@ -570,10 +650,7 @@ __global__ __launch_bounds__(kBlock) void light_kernel(DevScene S, const double*
     __shared__ double s_t[kShort * kBlock];
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
-    Stack stk;
-    stk.sn = s_n + threadIdx.x; stk.st = s_t + threadIdx.x;
-    stk.gn = spill_n ? spill_n + i : nullptr; stk.gt = spill_t ? spill_t + i : nullptr;
-    stk.stride = gridDim.x * kBlock; stk.sp = 0;
+    Stack stk = make_stack(s_n, s_t, threadIdx.x, i, spill_n, spill_t, gridDim.x * kBlock);
     Cnt<false> C;
     V3 o = load3(rays + 6 * (size_t)i), d = load3(rays + 6 * (size_t)i + 3);
     uint32_t nh = 0;
@@ -602,14 +679,60 @@ __global__ void fp64_probe_kernel(const double* a, const double* b, double* out,
 }
 
 // ------------------------------------------------------------- launch ----
-hipError_t launch_path(const DevScene& S, const KParams& P, uint32_t n_slots, double* out, int32_t* hit_ids,
-                       unsigned long long* stats, uint32_t* spill_n, double* spill_t, hipStream_t st) {
-    dim3 grid(n_slots), block(kBlock);
+// Persistent grid: the number of path-kernel waves resident on the device at
+// once (occupancy x CUs), capped by the number of wave-tiles.  Extra waves
+// would only find the queue drained.
+hipError_t path_grid(bool stats, bool hits, uint32_t n_units, uint32_t* grid) {
+    int dev = 0, cus = 0, per_cu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return e;
+    const void* k = stats ? (hits ? (const void*)path_kernel<true, true> : (const void*)path_kernel<true, false>)
+                          : (hits ? (const void*)path_kernel<false, true> : (const void*)path_kernel<false, false>);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kWave, 0);
+    if (e != hipSuccess) return e;
+    const uint64_t g = (uint64_t)std::max(per_cu, 1) * (uint64_t)std::max(cus, 1);
+    *grid = (uint32_t)std::min<uint64_t>(g, std::max<uint32_t>(n_units, 1u));
+    return hipSuccess;
+}
+
+hipError_t launch_path(const DevScene& S, const KParams& P, const PathWork& W, double* out, int32_t* hit_ids,
+                       unsigned long long* stats, hipStream_t st) {
+    if (P.chunks == 0 || (P.chunks > 1 && !W.part) || !W.queue || !W.ring || W.grid == 0) return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(W.queue, 0, sizeof(uint32_t), st);
+    if (e != hipSuccess) return e;
+    dim3 grid(W.grid), block(kWave);
     const bool ST = stats != nullptr, HIT = hit_ids != nullptr;
-    if (ST && HIT) hipLaunchKernelGGL((path_kernel<true, true>), grid, block, 0, st, S, P, out, hit_ids, stats, spill_n, spill_t);
-    else if (ST) hipLaunchKernelGGL((path_kernel<true, false>), grid, block, 0, st, S, P, out, hit_ids, stats, spill_n, spill_t);
-    else if (HIT) hipLaunchKernelGGL((path_kernel<false, true>), grid, block, 0, st, S, P, out, hit_ids, stats, spill_n, spill_t);
-    else hipLaunchKernelGGL((path_kernel<false, false>), grid, block, 0, st, S, P, out, hit_ids, stats, spill_n, spill_t);
+#define RT_LAUNCH(a, b)                                                                                   \
+    hipLaunchKernelGGL((path_kernel<a, b>), grid, block, 0, st, S, P, out, W.part, hit_ids, stats, W.spill_n, \
+                       W.spill_t, W.queue, W.ring)
+    if (ST && HIT) RT_LAUNCH(true, true);
+    else if (ST) RT_LAUNCH(true, false);
+    else if (HIT) RT_LAUNCH(false, true);
+    else RT_LAUNCH(false, false);
+#undef RT_LAUNCH
+    e = hipGetLastError();
+    if (e != hipSuccess || P.chunks == 1) return e;
+    return launch_reduce_chunks(W.part, out, P, st);
+}
+
+// Chunk partial sums -> per-pixel mean: ((p0 + p1) + ... + pK-1) / spp, in
+// chunk order (the oracle's chunked iterative form sums identically).
+__global__ void reduce_chunks_kernel(const double* __restrict__ part, double* __restrict__ out, uint32_t n_slots,
+                                     uint32_t chunks, double spp) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (slot, pixel-in-tile, channel)
+    if (i >= (uint64_t)n_slots * kBlock * 3) return;
+    const uint64_t slot = i / (kBlock * 3), rem = i % (kBlock * 3);
+    const double* p = part + slot * chunks * (kBlock * 3) + rem;
+    double s = p[0];
+    for (uint32_t k = 1; k < chunks; ++k) s = s + p[(uint64_t)k * kBlock * 3];
+    out[i] = s / spp;
+}
+
+hipError_t launch_reduce_chunks(const double* part, double* out, const KParams& P, hipStream_t st) {
+    const uint64_t n = (uint64_t)P.n_slots * kBlock * 3;
+    hipLaunchKernelGGL(reduce_chunks_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, out,
+                       P.n_slots, P.chunks, (double)P.spp);
     return hipGetLastError();
 }
 hipError_t launch_intersect(const DevScene& S, const double* rays, uint32_t n, rt_hit* out, uint32_t* spill_n,

@@ -110,12 +110,12 @@ RT_D bool gen_bool(Rng& r, double p) {  // Bernoulli
 
 // ------------------------------------------------------------- counters ---
 struct Counters {
-    uint32_t segments, aabb, tri, shape, shaded, lq, lhits, paths;
+    uint32_t segments, aabb, tri, shape, shaded, lq, lhits, paths, steps;
 };
 template <bool ON>
 struct Cnt {
     Counters c;
-    RT_D void zero() { if (ON) { c = Counters{0, 0, 0, 0, 0, 0, 0, 0}; } }
+    RT_D void zero() { if (ON) { c = Counters{0, 0, 0, 0, 0, 0, 0, 0, 0}; } }
     RT_D void segment() { if (ON) c.segments++; }
     RT_D void aabb(uint32_t n = 1) { if (ON) c.aabb += n; }
     RT_D void tri() { if (ON) c.tri++; }
@@ -124,6 +124,7 @@ struct Cnt {
     RT_D void lq() { if (ON) c.lq++; }
     RT_D void lhit() { if (ON) c.lhits++; }
     RT_D void path() { if (ON) c.paths++; }
+    RT_D void step() { if (ON) c.steps++; }
 };
 
 // ------------------------------------------------------ exact division ----

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RT_API_VERSION 1
+#define RT_API_VERSION 2
 
 typedef enum rt_error {
     RT_OK = 0,
@@ -133,6 +133,9 @@ typedef struct rt_stats {
     uint64_t light_hits;       /* callbacks of intersect_lights                  */
     double   kernel_ms;        /* device time of the path kernel(s)              */
     double   total_ms;         /* wall time of rt_render incl. copies            */
+    uint64_t lane_steps;       /* regeneration-loop steps summed over lanes      */
+    uint64_t wave_steps;       /* 64 x (steps of the wave's longest lane): lane  */
+                               /* utilisation of the path loop = lane/wave steps */
 } rt_stats;
 
 /* Hit-id sentinels in the (pixel, sample, bounce) dump */
@@ -186,9 +189,20 @@ int rt_render(rt_scene* scene, const rt_render_params* params,
    asynchronously on `hip_stream` (NULL = default stream). */
 #define RT_TILE 16
 int rt_tiles_per_rank(const rt_render_params* params, uint32_t world, uint32_t* n_tiles_padded);
+/* The scene's per-call workspace (stack spill, chunk partials) is shared: one
+   scene renders on one stream at a time. */
 int rt_render_tiles_async(rt_scene* scene, const rt_render_params* params,
                           uint32_t rank, uint32_t world,
                           double* d_tile_rgb, void* hip_stream);
+
+/* Sample chunking of the work units: a pixel's spp samples are
+   rendered in `chunks` runs of `chunk_spp` consecutive samples by different
+   lanes; each run is summed in sample order from 0, the run sums are added in
+   run order and divided by spp.  A function of (width, height, spp) only, so the
+   image is identical for any rank count.  chunks == 1 is exactly main.rs:94-104's
+   sequential sum; otherwise the result differs from it by f64 reassociation only
+   (no replacement for main.rs; exposed so checkers can reproduce the order). */
+int rt_sample_chunks(const rt_render_params* params, uint32_t* chunks, uint32_t* chunk_spp);
 /* Work counters accumulated on the device by every rt_render_tiles_async call
    made with RT_FLAG_STATS since the last reset (synchronises the device). */
 int rt_read_stats(rt_scene* scene, rt_stats* out, int reset);

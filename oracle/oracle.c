@@ -1018,7 +1018,14 @@ static void fuzzy_ray(const Camera* c, uint32_t x, uint32_t y, Rng* r, V3* o, V3
 int oracle_render(const oracle_scene* s, const rt_render_params* p, int mode, int threads,
                   uint32_t row_begin, uint32_t row_end,
                   double* out, int32_t* hit_ids, rt_stats* stats) {
+    return oracle_render_chunked(s, p, mode, threads, row_begin, row_end, 0, out, hit_ids, stats);
+}
+
+int oracle_render_chunked(const oracle_scene* s, const rt_render_params* p, int mode, int threads,
+                          uint32_t row_begin, uint32_t row_end, uint32_t chunk_spp,
+                          double* out, int32_t* hit_ids, rt_stats* stats) {
     if (!s || !p || !out || p->width == 0 || p->height == 0) return RT_ERR_INVALID;
+    if (chunk_spp == 0 || chunk_spp > p->spp) chunk_spp = p->spp;
     if (row_end > p->height) row_end = p->height;
     if (row_begin >= row_end) return RT_ERR_INVALID;
     Camera cam = camera_new(p);
@@ -1039,7 +1046,7 @@ int oracle_render(const oracle_scene* s, const rt_render_params* p, int mode, in
 #endif
         Counters* c = &tc[tid];
         uint32_t x = (uint32_t)(idx % W), y = (uint32_t)(idx / W);
-        V3 sum = v3(0, 0, 0);
+        V3 sum = v3(0, 0, 0), run = v3(0, 0, 0);
         for (uint32_t smp = 0; smp < spp; ++smp) {
             Rng rng;
             rng_init(&rng, p->seed, idx, smp);
@@ -1051,7 +1058,11 @@ int oracle_render(const oracle_scene* s, const rt_render_params* p, int mode, in
             d = vnormalize(d); /* raytrace.rs:9 */
             c->paths++;
             V3 L = mode == 0 ? raytrace_impl(&cx, o, d, depth) : raytrace_iter(&cx, o, d);
-            sum = vadd(sum, L);
+            run = vadd(run, L);
+            if ((smp + 1) % chunk_spp == 0 || smp + 1 == spp) { /* end of a run (one run = main.rs's sum) */
+                sum = smp < chunk_spp ? run : vadd(sum, run);
+                run = v3(0, 0, 0);
+            }
         }
         vst(out + 3 * idx, vdivs(sum, (double)spp)); /* main.rs:104 before tonemapping */
     }

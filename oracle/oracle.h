@@ -47,6 +47,14 @@ int oracle_render(const oracle_scene* s, const rt_render_params* p, int mode,
                   int threads, uint32_t row_begin, uint32_t row_end,
                   double* out_mean_rgb, int32_t* opt_hit_ids, rt_stats* opt_stats);
 
+/* As oracle_render, with the device's chunked sample summation: a pixel's
+   samples are summed in runs of chunk_spp (each run from 0), the run sums are
+   added in order and the total divided by spp (render.hip reduce_chunks_kernel).
+   chunk_spp >= spp (or 0) is the plain sequential sum of main.rs:94-104. */
+int oracle_render_chunked(const oracle_scene* s, const rt_render_params* p, int mode,
+                          int threads, uint32_t row_begin, uint32_t row_end, uint32_t chunk_spp,
+                          double* out_mean_rgb, int32_t* opt_hit_ids, rt_stats* opt_stats);
+
 /* intersect(ray, primitives, +inf) for a batch (intersections.rs:42-62). */
 void oracle_intersect_rays(const oracle_scene* s, const double* rays, uint32_t n, rt_hit* out);
 /* Light::pdf for a batch of (pos, dir) (ray_sampler.rs:132-139). */

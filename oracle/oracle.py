@@ -37,6 +37,7 @@ def lib():
             "oracle_scene_bvh_dump": (u64, [vp, i32, vp, vp]),
             "oracle_scene_bvh_prim": (C.c_int64, [vp, i32, u64]),
             "oracle_render": (i32, [vp, vp, i32, i32, u32, u32, vp, vp, vp]),
+            "oracle_render_chunked": (i32, [vp, vp, i32, i32, u32, u32, u32, vp, vp, vp]),
             "oracle_intersect_rays": (None, [vp, vp, u32, vp]),
             "oracle_light_pdf_rays": (None, [vp, vp, u32, vp]),
             "oracle_aabb_intersects": (i32, [dp, dp, dp, dp, dp]),
@@ -103,8 +104,11 @@ class OracleScene:
             out.append(g)
             i += 1
 
-    def render(self, params, mode: int = 1, threads: int = 0, rows=None, hit_ids: bool = False):
+    def render(self, params, mode: int = 1, threads: int = 0, rows=None, hit_ids: bool = False,
+               chunk_spp: int = 0):
         """generate_image without tonemapping. mode 0 = recursive, 1 = iterative (device algorithm).
+        chunk_spp > 0 sums samples in runs of chunk_spp like the device's chunked
+        work units (oracle_render_chunked); 0 = the reference's sequential sum.
         Returns (image [H, W, 3], hit ids or None, stats dict)."""
         from_params = params.to_c()
         H, W = params.height, params.width
@@ -114,8 +118,8 @@ class OracleScene:
         if hit_ids:
             hits = np.full((H * W, params.spp, params.ray_depth), -2, np.int32)
         st = _stats_struct()
-        rc = lib().oracle_render(self._h, C.byref(from_params), mode, threads, r0, r1, img.ctypes.data,
-                                 None if hits is None else hits.ctypes.data, C.byref(st))
+        rc = lib().oracle_render_chunked(self._h, C.byref(from_params), mode, threads, r0, r1, chunk_spp,
+                                         img.ctypes.data, None if hits is None else hits.ctypes.data, C.byref(st))
         if rc != 0:
             raise RuntimeError(f"oracle_render failed: {rc}")
         return img, hits, {k: getattr(st, k) for k, _ in st._fields_}
@@ -150,7 +154,7 @@ def _stats_struct():
         _fields_ = [("paths", C.c_uint64), ("segments", C.c_uint64), ("aabb_tests", C.c_uint64),
                     ("tri_tests", C.c_uint64), ("shape_tests", C.c_uint64), ("shaded_hits", C.c_uint64),
                     ("light_queries", C.c_uint64), ("light_hits", C.c_uint64), ("kernel_ms", C.c_double),
-                    ("total_ms", C.c_double)]
+                    ("total_ms", C.c_double), ("lane_steps", C.c_uint64), ("wave_steps", C.c_uint64)]
     return rt_stats()
 
 

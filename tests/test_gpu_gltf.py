@@ -60,7 +60,7 @@ def test_atrium_intersect_random(atrium):
     gh, oh = g.intersect(rays), o.intersect(rays)
     assert np.array_equal(gh["prim"], oh["prim"])
     assert np.array_equal(gh.view(np.uint8), oh.view(np.uint8))
-    assert (gh["prim"] >= 0).mean() > 0.9   # closed atrium: almost every ray hits
+    assert (gh["prim"] >= 0).mean() > 0.75   # open-roofed atrium: upward rays may escape
 
 
 def test_atrium_light_pdf_random(atrium):

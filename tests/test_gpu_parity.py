@@ -31,8 +31,10 @@ def sink(rt, orc, scene_text):
 
 
 def _compare(gpu_scene, ora_scene, params):
+    from conftest import load_package
+    _, chunk_spp = load_package().sample_chunks(params)
     g_img, g_hits, g_st = gpu_scene.generate_image(params, hit_ids=True, stats=True)
-    o_img, o_hits, o_st = ora_scene.render(params, mode=1, hit_ids=True)
+    o_img, o_hits, o_st = ora_scene.render(params, mode=1, hit_ids=True, chunk_spp=chunk_spp)
     r_img, r_hits, _ = ora_scene.render(params, mode=0, hit_ids=True)
     assert np.array_equal(g_hits, o_hits), f"hit ids differ at {np.argwhere(g_hits != o_hits)[:5]}"
     assert np.array_equal(g_hits, r_hits)

@@ -163,6 +163,35 @@ def test_recursive_vs_iterative(rt, orc, scene_text, scene, over):
         assert sa[k] == sb[k]
 
 
+def test_chunked_sum_is_reassociation_only(rt, orc, scene_text):
+    """Chunked sample runs (the device's work units) change only the f64 summation order."""
+    desc, params = rt.parse_scene(scene_text("kitchen_sink.txt"))
+    params = params.replace(width=12, height=10, spp=7)
+    o = orc.OracleScene(desc)
+    seq, hs, ss = o.render(params, mode=1, hit_ids=True)
+    same, _, _ = o.render(params, mode=1, chunk_spp=7)
+    assert np.array_equal(seq, same)
+    for cs in (1, 2, 3, 5):
+        ch, hc, sc = o.render(params, mode=1, hit_ids=True, chunk_spp=cs)
+        assert np.array_equal(hs, hc) and ss == sc
+        np.testing.assert_allclose(ch, seq, rtol=1e-13, atol=1e-300)
+
+
+@pytest.mark.parametrize("w,h,spp,want", [
+    (1920, 1080, 256, (8, 32)),     # C2/C3: 16.6M work units
+    (3840, 2160, 1024, (2, 512)),   # C4
+    (256, 256, 64, (64, 1)),        # C1: capped at kMaxChunks
+    (48, 32, 4, (4, 1)),
+    (20, 12, 5, (3, 2)),            # 4 runs of 2 would leave one empty: trimmed to 3
+    (4000, 4000, 9, (1, 9)),        # already >= 16M pixels
+    (7, 3, 1, (1, 1)),
+])
+def test_sample_chunk_rule(rt, w, h, spp, want):
+    k, cs = rt.sample_chunks(rt.RenderParams(w, h, spp))
+    assert (k, cs) == want
+    assert (k - 1) * cs < spp <= k * cs   # no empty run, all samples covered
+
+
 def test_thread_count_independent(rt, orc, scene_text):
     desc, params = rt.parse_scene(scene_text("kitchen_sink.txt"))
     o = orc.OracleScene(desc)

@@ -1,0 +1,51 @@
+#!/bin/bash
+# One gpurun batch: GPU parity tests, C3 bench, kernel-trace profile, then PMC
+# passes (each counter group in its own run, no trace domains besides the
+# kernel dispatches).  Every GPU step has its own time limit and the chain stops
+# at the first failure.
+#   gpurun --timeout 1200 -- bash tools/gpu_batch.sh <tag> [steps...]
+# steps: tests c2 c3 prof2 prof3 pmc2 pmc3 occ2 (default: all)
+set -o pipefail
+cd "$(dirname "$0")/.." || exit 1
+export TMPDIR=/tmp
+TAG=${1:-run}; shift
+STEPS=${*:-"tests c3 prof3 pmc3 pmc2 occ2"}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+B="python3 bench.py"
+run() {  # run <name> <seconds> <cmd...>
+  local name=$1 secs=$2; shift 2
+  echo "[$(date +%T)] $name: $*"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[$(date +%T)] $name rc=$rc"; tail -3 "$OUT/$name.log"
+  return $rc
+}
+for s in $STEPS; do
+  case $s in
+    tests) run pytest_gpu 900 python3 -m pytest tests -m gpu -x -q || exit 1 ;;
+    c2)    run bench_c2 600 $B --workload C2 --steps 3 --warmup 1 || exit 1 ;;
+    c3)    run bench_c3 600 $B --workload C3 --steps 3 --warmup 1 || exit 1 ;;
+    prof2) run prof_c2 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c2" -o run \
+             -- $B --workload C2 --steps 2 --warmup 1 --no-cpu-baseline || exit 1 ;;
+    prof3) run prof_c3 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c3" -o run \
+             -- $B --workload C3 --steps 2 --warmup 1 --no-cpu-baseline || exit 1 ;;
+    pmc2|pmc3)
+      w=C${s#pmc}
+      run fetch_$w 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch_$w" -o run \
+        -- $B --workload $w --steps 1 --warmup 0 --no-cpu-baseline || exit 1
+      run write_$w 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write_$w" -o run \
+        -- $B --workload $w --steps 1 --warmup 0 --no-cpu-baseline || exit 1 ;;
+    occ2)  run occ_C2 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
+             --output-format csv -d "$OUT/occ_C2" -o run \
+             -- $B --workload C2 --steps 1 --warmup 0 --no-cpu-baseline || exit 1 ;;
+    lane2) run lane_C2 600 python3 tools/lane_util.py C2 256 256 64 32 8 || exit 1 ;;
+    lane3) run lane_C3 600 python3 tools/lane_util.py C3 64 64 32 8 || exit 1 ;;
+    var2|var3)  # every cpu-raytracing-rt_amd/build*/librt_amd.so variant at reduced spp
+      w=C${s#var}
+      run variants_$w 900 python3 tools/variants.py $w ${VAR_SPP:-64} cpu-raytracing-rt_amd/build*/librt_amd.so \
+        || exit 1 ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "[$(date +%T)] batch done"

@@ -1,26 +1,38 @@
-"""Time alternate builds of librt_amd.so on the C2 workload at reduced spp.
-usage: python tools/variants.py SPP lib1.so lib2.so ...  (each in its own process)"""
-import json, os, subprocess, sys
+"""Time alternate builds of librt_amd.so on a bench workload at reduced spp.
+usage: python tools/variants.py WORKLOAD SPP lib1.so lib2.so ...   (each lib in its own process)
+WORKLOAD is a bench.py workload name (C1, C2, C3, ...)."""
+import os
+import subprocess
+import sys
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 CHILD = r'''
-import os, sys, time, json
-sys.path.insert(0, os.path.join(sys.argv[1], "tests"))
+import os, sys, json
+root = sys.argv[1]
+sys.path.insert(0, os.path.join(root, "tests")); sys.path.insert(0, root)
+import torch  # one HIP runtime per process
 from conftest import load_package
+import bench
 rt = load_package()
-desc, params = rt.parse_scene(open(os.path.join(sys.argv[1], "scenes", "cornell.txt")).read())
+scene_file, W, H, spp, depth = bench.WORKLOADS[sys.argv[2]]
+desc, params = bench.load_workload(rt, scene_file, W, H, int(sys.argv[3]))
+if depth:
+    params = params.replace(ray_depth=depth)
 s = rt.Scene(desc)
-p = params.replace(width=1920, height=1080, spp=int(sys.argv[2]))
-_, _, st = s.generate_image(p, stats=True)
+_, _, st = s.generate_image(params, stats=True)
 ks = []
 for i in range(3):
-    _, _, st2 = s.generate_image(p)
+    _, _, st2 = s.generate_image(params)
     ks.append(st2["kernel_ms"])
-print(json.dumps({"lib": os.environ["RT_AMD_LIB"], "kernel_ms": ks, "Mseg_s": st["segments"] / min(ks) / 1e3,
-                  "segments": st["segments"]}))
+print(json.dumps({"lib": os.environ["RT_AMD_LIB"], "workload": sys.argv[2], "spp": params.spp, "kernel_ms": ks,
+                  "Mseg_s": st["segments"] / min(ks) / 1e3, "segments": st["segments"]}))
 '''
-spp = sys.argv[1]
-for lib in sys.argv[2:]:
+wl, spp = sys.argv[1], sys.argv[2]
+rc = 0
+for lib in sys.argv[3:]:
     env = dict(os.environ, RT_AMD_LIB=os.path.abspath(lib))
-    r = subprocess.run([sys.executable, "-c", CHILD, os.path.dirname(HERE), spp], env=env, capture_output=True,
-                       text=True, timeout=300)
+    r = subprocess.run([sys.executable, "-c", CHILD, os.path.dirname(HERE), wl, spp], env=env, capture_output=True,
+                       text=True, timeout=600)
     print(r.stdout.strip() or r.stderr[-2000:], flush=True)
+    rc = rc or r.returncode
+sys.exit(rc)
