@@ -190,16 +190,31 @@ int ensure_spill(rt_scene* s, uint64_t lanes) {
     return RT_OK;
 }
 
+// Register budget of the path kernel for this scene.  Large BVHs make the loop
+// latency-bound on dependent node loads, where a 4th wave per SIMD hides more
+// than its register spill costs (C3: -9%); small scenes are VALU-bound and run
+// best at 3 (C2: +2% at 4).  RT_WAVES=3|4 forces one (tests, tuning).
+uint32_t path_waves(const rt_scene* s) {
+    if (const char* e = std::getenv("RT_WAVES")) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v == 3 || v == 4) return (uint32_t)v;
+    }
+    uint64_t nodes = 0;
+    for (int k = 0; k < 6; ++k) nodes += s->info.bvh_nodes[k];
+    return nodes > kDeepSceneNodes ? 4u : 3u;
+}
+
 // Workspace of one path-kernel launch: persistent grid size, then the spill,
 // ring and chunk-partial buffers sized for it (all grow-only, scene-owned).
 int prepare_path(rt_scene* s, const KParams& k, bool stats, bool hits, PathWork& W) {
     const uint64_t n_units = (uint64_t)k.n_slots * k.chunks * 4;
     if (n_units >= (1ull << 31)) return set_error(RT_ERR_INVALID, "frame too large for one launch");
     std::memset(&W, 0, sizeof(W));
-    HIP_TRY(path_grid(stats, hits, (uint32_t)n_units, &W.grid));
+    W.waves = path_waves(s);
+    HIP_TRY(path_grid(stats, hits, W.waves, (uint32_t)n_units, &W.grid));
     int rc;
     if ((rc = ensure_spill(s, (uint64_t)W.grid * 64)) || (rc = ensure_part(s, k))) return rc;
-    if (!s->queue) HIP_TRY(hipMalloc(&s->queue, sizeof(uint32_t)));
+    if (!s->queue) HIP_TRY(hipMalloc(&s->queue, kQueueWords * sizeof(uint32_t)));
     const size_t ring_need = (size_t)W.grid * kRingRows * 64 * 3;
     if (ring_need > s->ring_entries) {
         if (s->ring) (void)hipFree(s->ring);

@@ -47,6 +47,7 @@ inline void sample_chunks(uint32_t W, uint32_t H, uint32_t spp, uint32_t& chunks
 
 // Device workspace of one path-kernel launch (owned by the scene).
 struct PathWork {
+    uint32_t waves;       // register budget of the kernel instance: 3 or 4 waves/SIMD
     uint32_t grid;        // persistent waves (path_grid)
     uint32_t* queue;      // wave-tile counter, zeroed by launch_path
     double* ring;         // [grid][kRing=8][64][3] finished-path radiance
@@ -55,8 +56,10 @@ struct PathWork {
     double* spill_t;
 };
 constexpr uint32_t kRingRows = 8;   // render.hip kRing
+constexpr uint64_t kDeepSceneNodes = 4096;  // BVH nodes above which the 4-wave kernel runs
+constexpr size_t kQueueWords = 16;  // wave-tile counter (word 0), padded to a 64-B line
 
-hipError_t path_grid(bool stats, bool hits, uint32_t n_units, uint32_t* grid);
+hipError_t path_grid(bool stats, bool hits, uint32_t waves, uint32_t n_units, uint32_t* grid);
 hipError_t launch_path(const DevScene& S, const KParams& P, const PathWork& W, double* out, int32_t* hit_ids,
                        unsigned long long* stats, hipStream_t st);
 hipError_t launch_reduce_chunks(const double* part, double* out, const KParams& P, hipStream_t st);

@@ -27,9 +27,6 @@
 namespace rt {
 
 constexpr int kBlock = 256;
-#ifndef RT_MIN_WAVES
-#define RT_MIN_WAVES 3  // path_kernel register budget: 3 waves/SIMD measured best
-#endif
 constexpr int kShort = kMaxBvhDepthShort;
 
 // ---------------------------------------------------------------- stack ---
@@ -503,8 +500,10 @@ RT_D void wave_flush(const Cnt<ST>& C, unsigned long long* stats, uint32_t wave_
 // (main.rs:94-104; bit-identical to the sequential sum when chunks == 1).
 constexpr int kRing = (int)kRingRows;
 
-template <bool ST, bool HIT>
-__global__ __launch_bounds__(kWave, RT_MIN_WAVES) void path_kernel(DevScene S, KParams P, double* __restrict__ out,
+// WAVES = minimum waves per SIMD the register budget must allow (3: 168 VGPRs,
+// 4: 128 VGPRs + spill); chosen per scene by the host.
+template <bool ST, bool HIT, int WAVES>
+__global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene S, KParams P, double* __restrict__ out,
                                                      double* __restrict__ part, int32_t* __restrict__ hit_ids,
                                                      unsigned long long* __restrict__ stats, uint32_t* spill_n,
                                                      double* spill_t, uint32_t* __restrict__ queue,
@@ -682,14 +681,24 @@ __global__ void fp64_probe_kernel(const double* a, const double* b, double* out,
 // Persistent grid: the number of path-kernel waves resident on the device at
 // once (occupancy x CUs), capped by the number of wave-tiles.  Extra waves
 // would only find the queue drained.
-hipError_t path_grid(bool stats, bool hits, uint32_t n_units, uint32_t* grid) {
+namespace {
+using PathFn = void (*)(DevScene, KParams, double*, double*, int32_t*, unsigned long long*, uint32_t*, double*,
+                        uint32_t*, double*);
+PathFn path_fn(bool stats, bool hits, uint32_t waves) {
+    static const PathFn tab[8] = {path_kernel<false, false, 3>, path_kernel<false, false, 4>,
+                                  path_kernel<false, true, 3>,  path_kernel<false, true, 4>,
+                                  path_kernel<true, false, 3>,  path_kernel<true, false, 4>,
+                                  path_kernel<true, true, 3>,   path_kernel<true, true, 4>};
+    return tab[(stats ? 4 : 0) + (hits ? 2 : 0) + (waves == 4 ? 1 : 0)];
+}
+}  // namespace
+
+hipError_t path_grid(bool stats, bool hits, uint32_t waves, uint32_t n_units, uint32_t* grid) {
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e != hipSuccess) return e;
-    const void* k = stats ? (hits ? (const void*)path_kernel<true, true> : (const void*)path_kernel<true, false>)
-                          : (hits ? (const void*)path_kernel<false, true> : (const void*)path_kernel<false, false>);
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kWave, 0);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)path_fn(stats, hits, waves), kWave, 0);
     if (e != hipSuccess) return e;
     const uint64_t g = (uint64_t)std::max(per_cu, 1) * (uint64_t)std::max(cus, 1);
     *grid = (uint32_t)std::min<uint64_t>(g, std::max<uint32_t>(n_units, 1u));
@@ -699,18 +708,11 @@ hipError_t path_grid(bool stats, bool hits, uint32_t n_units, uint32_t* grid) {
 hipError_t launch_path(const DevScene& S, const KParams& P, const PathWork& W, double* out, int32_t* hit_ids,
                        unsigned long long* stats, hipStream_t st) {
     if (P.chunks == 0 || (P.chunks > 1 && !W.part) || !W.queue || !W.ring || W.grid == 0) return hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync(W.queue, 0, sizeof(uint32_t), st);
+    if (W.waves != 3 && W.waves != 4) return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(W.queue, 0, kQueueWords * sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
-    dim3 grid(W.grid), block(kWave);
-    const bool ST = stats != nullptr, HIT = hit_ids != nullptr;
-#define RT_LAUNCH(a, b)                                                                                   \
-    hipLaunchKernelGGL((path_kernel<a, b>), grid, block, 0, st, S, P, out, W.part, hit_ids, stats, W.spill_n, \
-                       W.spill_t, W.queue, W.ring)
-    if (ST && HIT) RT_LAUNCH(true, true);
-    else if (ST) RT_LAUNCH(true, false);
-    else if (HIT) RT_LAUNCH(false, true);
-    else RT_LAUNCH(false, false);
-#undef RT_LAUNCH
+    hipLaunchKernelGGL(path_fn(stats != nullptr, hit_ids != nullptr, W.waves), dim3(W.grid), dim3(kWave), 0, st, S,
+                       P, out, W.part, hit_ids, stats, W.spill_n, W.spill_t, W.queue, W.ring);
     e = hipGetLastError();
     if (e != hipSuccess || P.chunks == 1) return e;
     return launch_reduce_chunks(W.part, out, P, st);

@@ -44,10 +44,13 @@ def test_room_deep_fov(room):
     _compare(g, o, params.replace(width=17, height=23, spp=3, ray_depth=20, fov=1.4, seed=11))
 
 
-def test_atrium(atrium):
+@pytest.mark.parametrize("waves", ["3", "4"])
+def test_atrium(atrium, monkeypatch, waves):
+    monkeypatch.setenv("RT_WAVES", waves)
     desc, params, g, o = atrium
     img, _, st = _compare(g, o, params)
     assert st["tri_tests"] > 0 and img.max() > 0
+    assert st["lane_steps"] <= st["wave_steps"]
 
 
 def test_atrium_intersect_random(atrium):

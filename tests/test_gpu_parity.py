@@ -60,6 +60,23 @@ def test_cornell_small(cornell):
     _compare(g, o, params.replace(width=48, height=40, spp=4))
 
 
+@pytest.mark.parametrize("waves", ["3", "4"])
+def test_both_register_budgets(cornell, monkeypatch, waves):
+    """Both path-kernel instances (3 and 4 waves/SIMD) are bit-exact (host picks per scene)."""
+    monkeypatch.setenv("RT_WAVES", waves)
+    desc, params, g, o = cornell
+    _compare(g, o, params.replace(width=40, height=24, spp=3, seed=3))
+
+
+@pytest.mark.parametrize("chunk_spp", ["37", "1"])
+def test_sample_ring_wraps(sink, monkeypatch, chunk_spp):
+    """Long sample runs: the 8-row commit ring wraps many times (37 + 3 rows per
+    wave-tile); run length 1: one row per wave-tile, 40 partials per pixel."""
+    monkeypatch.setenv("RT_CHUNK_SPP", chunk_spp)
+    desc, params, g, o = sink
+    _compare(g, o, params.replace(width=20, height=12, spp=40, ray_depth=8, seed=17))
+
+
 def test_cornell_seed_changes_image(cornell):
     desc, params, g, o = cornell
     p = params.replace(width=32, height=32, spp=2)

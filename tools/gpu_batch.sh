@@ -39,6 +39,12 @@ for s in $STEPS; do
     occ2)  run occ_C2 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
              --output-format csv -d "$OUT/occ_C2" -o run \
              -- $B --workload C2 --steps 1 --warmup 0 --no-cpu-baseline || exit 1 ;;
+    ctrs)  run counters 300 rocprofv3 -L || exit 1 ;;
+    mix2|mix3)  # SQ instruction mix + stall cycles of the path kernel (one SQ pass, 8 slots)
+      w=C${s#mix}
+      run mix_$w 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS \
+        SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_BUSY_CYCLES --output-format csv -d "$OUT/mix_$w" -o run \
+        -- $B --workload $w --steps 1 --warmup 0 --no-cpu-baseline --no-pmc || exit 1 ;;
     lane2) run lane_C2 600 python3 tools/lane_util.py C2 256 256 64 32 8 || exit 1 ;;
     lane3) run lane_C3 600 python3 tools/lane_util.py C3 64 64 32 8 || exit 1 ;;
     var2|var3)  # every cpu-raytracing-rt_amd/build*/librt_amd.so variant at reduced spp
