@@ -112,6 +112,7 @@ EXPORTS = {
     "rt_render_tiles_async": (C.c_int, [C.c_void_p, C.POINTER(rt_render_params), C.c_uint32, C.c_uint32,
                                         C.c_void_p, C.c_void_p]),
     "rt_read_stats": (C.c_int, [C.c_void_p, C.POINTER(rt_stats), C.c_int]),
+    "rt_read_raw_stats": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
     "rt_unpack_tiles_async": (C.c_int, [C.POINTER(rt_render_params), C.c_uint32, C.c_void_p, C.c_void_p,
                                         C.c_void_p]),
     "rt_intersect_rays": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]),
@@ -406,6 +407,12 @@ class Scene:
         st = rt_stats()
         _check(lib().rt_read_stats(self._h, C.byref(st), 1 if reset else 0))
         return st.as_dict()
+
+    def read_raw_stats(self, n: int = 32) -> np.ndarray:
+        """Raw device counter words (diagnostics; rt_read_raw_stats)."""
+        out = np.zeros(n, np.uint64)
+        _check(lib().rt_read_raw_stats(self._h, out.ctypes.data_as(C.c_void_p), n))
+        return out
 
 
 def tile_layout(width: int, height: int, world: int):

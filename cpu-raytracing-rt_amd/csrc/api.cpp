@@ -287,8 +287,8 @@ int rt_scene_create(const rt_scene_desc* desc, rt_scene** out) {
         s->info.bvh_nodes[k] = hs.bvh[k].nodes.size();
         s->info.bvh_depth[k] = hs.bvh[k].depth;
     }
-    HIP_TRY(hipMalloc(&s->d_stats, kNStats * sizeof(unsigned long long)));
-    HIP_TRY(hipMemset(s->d_stats, 0, kNStats * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&s->d_stats, kStatsWords * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(s->d_stats, 0, kStatsWords * sizeof(unsigned long long)));
     s->info.n_planes = d.n_planes;
     s->info.n_boxes = d.boxes.n_prims;
     s->info.n_ellipsoids = d.ells.n_prims;
@@ -347,7 +347,15 @@ int rt_read_stats(rt_scene* s, rt_stats* out, int reset) {
     std::memset(out, 0, sizeof(*out));
     int rc = copy_stats(s, out);
     if (rc) return rc;
-    if (reset) HIP_TRY(hipMemset(s->d_stats, 0, kNStats * sizeof(unsigned long long)));
+    if (reset) HIP_TRY(hipMemset(s->d_stats, 0, kStatsWords * sizeof(unsigned long long)));
+    return RT_OK;
+}
+
+int rt_read_raw_stats(rt_scene* s, uint64_t* out, uint32_t n) {
+    if (!s || !out || n > (uint32_t)kStatsWords) return set_error(RT_ERR_INVALID, "scene/out NULL or n > 32");
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(out, s->d_stats, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return RT_OK;
 }
 
@@ -382,7 +390,7 @@ int rt_render(rt_scene* s, const rt_render_params* p, double* out_mean_rgb, int3
     HIP_TRY(img.alloc(npx * 3));
     const uint64_t nhits = npx * p->spp * p->ray_depth;
     if (want_hits) HIP_TRY(hits.alloc(nhits));
-    if (want_stats) HIP_TRY(hipMemset(s->d_stats, 0, kNStats * sizeof(unsigned long long)));
+    if (want_stats) HIP_TRY(hipMemset(s->d_stats, 0, kStatsWords * sizeof(unsigned long long)));
     hipEvent_t e0, e1;
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));

@@ -28,11 +28,44 @@ namespace rt {
 
 constexpr int kBlock = 256;
 constexpr int kShort = kMaxBvhDepthShort;
+#ifndef RT_LEAF_BATCH
+#define RT_LEAF_BATCH 16  // lanes waiting at leaves before the wave tests primitives (bvh_closest)
+#endif
+constexpr int kLeafBatch = RT_LEAF_BATCH;
 
 // ---------------------------------------------------------------- stack ---
 // LDS short stack laid out per wave: [wave][slot][lane], so consecutive lanes
 // hit consecutive banks for any block size.
 constexpr int kWave = 64;
+
+// ---- diagnostics: wave cycles per code region (tools/phases.py) ----------
+// Only in -DRT_PHASES builds: s_memtime deltas, added once per wave by the
+// first active lane into LDS, flushed to raw stats words 16..23 (kPhase*).
+// The last four words count BVH traversal-loop iterations (wave-level and
+// summed over lanes) and primitive tests (wave-level inner-loop trips and
+// lane-level tests): their ratios are the loop's SIMD utilisation.
+enum { kPhAssign, kPhIntersect, kPhLightSample, kPhLightPdf, kPhSegment, kPhCommit, kPhTile,
+       kPhTravWave, kPhTravLane, kPhLeafWave, kPhLeafLane, kPhN };
+#ifdef RT_PHASES
+__shared__ unsigned long long g_phase[kPhN];
+#define PH_T() __builtin_amdgcn_s_memtime()
+#define PH_FIRST() (__lane_id() == (unsigned)__builtin_amdgcn_readfirstlane(__lane_id()))
+// (atomics, so the compiler cannot keep a lane-private copy across iterations)
+#define PH_ADD(k, t0)                                                                        \
+    do {                                                                                     \
+        const unsigned long long dt_ = PH_T() - (t0);                                        \
+        if (PH_FIRST()) atomicAdd(&g_phase[k], dt_);                                         \
+    } while (0)
+#define PH_COUNT(kw, kl)                                                                     \
+    do {                                                                                     \
+        if (PH_FIRST()) atomicAdd(&g_phase[kw], 1ull);                                       \
+        atomicAdd(&g_phase[kl], 1ull);                                                       \
+    } while (0)
+#else
+#define PH_T() 0ull
+#define PH_ADD(k, t0) ((void)(t0))
+#define PH_COUNT(kw, kl) ((void)0)
+#endif
 struct Stack {
     uint32_t* sn;        // LDS node slots, stride kWave
     double* st;          // LDS entry-t slots, stride kWave
@@ -105,21 +138,39 @@ RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stack& S, Cnt
     double best = INFINITY;
     uint32_t node = 0;
     S.sp = 0;
+    // Deferred leaves: a lane that reaches a leaf waits there while the other
+    // lanes keep stepping through internal nodes; the wave tests leaf
+    // primitives once >= kLeafBatch lanes wait (or every live lane does), so
+    // the primitive loop runs with many lanes instead of a few.  Each lane's
+    // own sequence of visits, tests, `best` updates and pruning is unchanged
+    // (the reference's order, bvh.rs:151-210) — only when it runs moves.
+    uint32_t cnt = B.nodes[0].count;
+    bool live = true;
     for (;;) {
-        const DevNode& n = B.nodes[node];
-        const uint32_t cnt = n.count, start = n.start;
-        for (uint32_t i = start; i < start + cnt; ++i) {
-            double t, u = 0.0, v = 0.0;
-            uint32_t aux = 0;
-            bool h;
-            if (KIND == 3) { C.tri(); h = tri_uvt(B.tris[i], o, d, u, v, t); }
-            else { C.shape(); h = shape_closest<KIND>(B.shapes[i], o, d, rc, t, aux); }
-            if (h && (!valid || t < best)) {  // update_best_intersection (bvh.rs:213-222)
-                valid = true; best = t; bu = u; bv = v; bprim = i; baux = aux;
+        const uint64_t lv = __ballot(live);
+        if (lv == 0) break;
+        const uint64_t at_leaf = __ballot(live && cnt != 0);
+        const bool do_leaves = at_leaf == lv || __popcll(at_leaf) >= kLeafBatch;
+        PH_COUNT(kPhTravWave, kPhTravLane);
+        bool next = false;  // this lane finished its current node and pops
+        if (do_leaves) {
+            if (live && cnt != 0) {
+                const uint32_t start = B.nodes[node].start;
+                for (uint32_t i = start; i < start + cnt; ++i) {
+                    PH_COUNT(kPhLeafWave, kPhLeafLane);
+                    double t, u = 0.0, v = 0.0;
+                    uint32_t aux = 0;
+                    bool h;
+                    if (KIND == 3) { C.tri(); h = tri_uvt(B.tris[i], o, d, u, v, t); }
+                    else { C.shape(); h = shape_closest<KIND>(B.shapes[i], o, d, rc, t, aux); }
+                    if (h && (!valid || t < best)) {  // update_best_intersection (bvh.rs:213-222)
+                        valid = true; best = t; bu = u; bv = v; bprim = i; baux = aux;
+                    }
+                }
+                next = true;
             }
-        }
-        const int32_t left = n.left;
-        if (left >= 0) {
+        } else if (live && cnt == 0) {  // internal node (count 0 <=> children)
+            const DevNode& n = B.nodes[node];
             double lt = 0.0, rt2 = 0.0;
             C.aabb(2);
             bool lh = aabb_hit(load3(n.lmin), load3(n.lmax), o, d, rc, lt);
@@ -127,21 +178,28 @@ RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stack& S, Cnt
             const double bt = best;  // +inf when no hit yet
             const double li = lh ? (lt < bt ? lt : bt) : bt;
             const double ri = rh ? (rt2 < bt ? rt2 : bt) : bt;
+            const uint32_t left = (uint32_t)n.left, right = (uint32_t)n.right;
             if (li < bt) {
                 if (ri < bt) {
-                    if (li < ri) { S.push((uint32_t)n.right, ri); node = (uint32_t)left; }
-                    else { S.push((uint32_t)left, li); node = (uint32_t)n.right; }
-                } else node = (uint32_t)left;
-                continue;
-            } else if (ri < bt) { node = (uint32_t)n.right; continue; }
+                    if (li < ri) { S.push(right, ri); node = left; }
+                    else { S.push(left, li); node = right; }
+                } else node = left;
+                cnt = B.nodes[node].count;
+            } else if (ri < bt) {
+                node = right;
+                cnt = B.nodes[node].count;
+            } else next = true;
         }
-        bool found = false;
-        while (S.sp > 0) {
-            uint32_t nn; double tt;
-            S.pop(nn, tt);
-            if (tt < best) { node = nn; found = true; break; }
+        if (next) {  // resume from the stack: far children still closer than best
+            bool found = false;
+            while (S.sp > 0) {
+                uint32_t nn; double tt;
+                S.pop(nn, tt);
+                if (tt < best) { node = nn; found = true; break; }
+            }
+            if (found) cnt = B.nodes[node].count;
+            else live = false;
         }
-        if (!found) break;
     }
     if (valid) bt_out = best;
     return valid;
@@ -403,7 +461,10 @@ RT_D bool segment(const DevScene& S, const KParams& P, const Scales& sc, PathSta
                   Stack& stk, Cnt<ST>& C, int32_t& hit_gid) {
     Hit h; uint32_t mat; int32_t gid;
     C.segment();
-    if (!scene_intersect<ST>(S, ps.o, ps.d, stk, C, h, mat, gid)) {
+    const unsigned long long ph0 = PH_T();
+    const bool hit = scene_intersect<ST>(S, ps.o, ps.d, stk, C, h, mat, gid);
+    PH_ADD(kPhIntersect, ph0);
+    if (!hit) {
         hit_gid = RT_HIT_MISS;
         ps.L = ps.L + mul(ps.T, load3(P.bg));
         return false;
@@ -418,11 +479,20 @@ RT_D bool segment(const DevScene& S, const KParams& P, const Scales& sc, PathSta
         const bool empty = S.n_lights == 0;
         V3 dir;
         if (empty || gen_bool(rng, 0.5)) dir = cosine_sample(h.ns, rng);   // Mix::sample (ray_sampler.rs:87-93)
-        else dir = light_sample(S, pos, rng, sc);
+        else {
+            const unsigned long long ph1 = PH_T();
+            dir = light_sample(S, pos, rng, sc);
+            PH_ADD(kPhLightSample, ph1);
+        }
         const double cs = dot(dir, h.ns);
         if (cs <= 0.0) return false;
-        double pdf = empty ? cosine_pdf(h.ns, dir)
-                           : (cosine_pdf(h.ns, dir) + light_pdf<ST>(S, pos, dir, stk, C)) / 2.0;  // Mix::pdf
+        double lp = 0.0;
+        if (!empty) {
+            const unsigned long long ph2 = PH_T();
+            lp = light_pdf<ST>(S, pos, dir, stk, C);
+            PH_ADD(kPhLightPdf, ph2);
+        }
+        double pdf = empty ? cosine_pdf(h.ns, dir) : (cosine_pdf(h.ns, dir) + lp) / 2.0;  // Mix::pdf
         if (pdf == 0.0) return false;
         V3 w = v3(((cs * col.x) / kPi) / pdf, ((cs * col.y) / kPi) / pdf, ((cs * col.z) / kPi) / pdf);
         ps.T = mul(ps.T, w);
@@ -521,7 +591,12 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene S, KParams 
     const uint64_t below = (1ull << lane) - 1ull;
     Cnt<ST> C;
     C.zero();
+#ifdef RT_PHASES
+    if (lane < kPhN) g_phase[lane] = 0;
+    __syncthreads();
+#endif
     for (;;) {  // wave-tiles; every wave leaves once the queue passes n_units
+        const unsigned long long ph_tile = PH_T();
         uint32_t u = 0;
         if (lane == 0) u = atomicAdd(queue, 1u);
         const uint32_t unit = __builtin_amdgcn_readfirstlane(u);
@@ -547,6 +622,7 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene S, KParams 
             // hand the next units to idle lanes, in lane order, inside the ring window
             const uint32_t limit = min(total, (base + kRing) * kWave);
             const uint64_t idle = __ballot(!busy);
+            const unsigned long long ph_a = PH_T();
             if (next < limit && idle) {
                 const uint32_t k = (uint32_t)__popcll(idle & below);
                 if (!busy && next + k < limit) {
@@ -576,13 +652,16 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene S, KParams 
                 }
                 next = min(limit, next + (uint32_t)__popcll(idle));
             }
+            PH_ADD(kPhAssign, ph_a);
             // one segment of every live path
             if (busy) {
                 C.step();
                 bool cont = false;
                 if (b < depth) {
                     int32_t g;
+                    const unsigned long long ph_s = PH_T();
                     cont = segment<ST>(S, P, sc, ps, rng, stk, C, g);
+                    PH_ADD(kPhSegment, ph_s);
                     if (HIT) hit_ids[(pixel * P.spp + s) * depth + b] = g;
                     ++b;
                 }
@@ -597,6 +676,7 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene S, KParams 
             }
             ++witers;
             // commit complete rows in sample order (ring stores visible to the wave)
+            const unsigned long long ph_c = PH_T();
             __syncthreads();
             while (base < nrows && s_cnt[base % kRing] == (uint32_t)kWave) {
                 const double* rp = ring + ((uint64_t)(base % kRing) * kWave + lane) * 3;
@@ -606,6 +686,7 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene S, KParams 
                 __syncthreads();
                 ++base;
             }
+            PH_ADD(kPhCommit, ph_c);
             if (base >= nrows) break;
         }
         const uint32_t lx = (quad & 1u) * 8u + (lane & 7u), ly = (quad >> 1) * 8u + (lane >> 3);
@@ -616,7 +697,11 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene S, KParams 
         o[0] = res.x; o[1] = res.y; o[2] = res.z;
         wave_flush<ST>(C, stats, witers);
         C.zero();
+        PH_ADD(kPhTile, ph_tile);
     }
+#ifdef RT_PHASES
+    if (ST && lane < kPhN) atomicAdd(&stats[kPhaseWord0 + lane], g_phase[lane]);
+#endif
 }
 
 __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S, const double* __restrict__ rays, uint32_t n,

@@ -45,6 +45,19 @@ for s in $STEPS; do
       run mix_$w 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS \
         SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_BUSY_CYCLES --output-format csv -d "$OUT/mix_$w" -o run \
         -- $B --workload $w --steps 1 --warmup 0 --no-cpu-baseline --no-pmc || exit 1 ;;
+    eff2|eff3)  # lane efficiency + f64/int mix (SQ pass), then L2 hit rate + L1->L2 latency (TCC/TCP pass)
+      w=C${s#eff}
+      run eff_$w 600 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU_FMA_F64 \
+        SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 \
+        --output-format csv -d "$OUT/eff_$w" -o run \
+        -- $B --workload $w --steps 1 --warmup 0 --no-cpu-baseline --no-pmc || exit 1
+      run l2_$w 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum \
+        --output-format csv -d "$OUT/l2_$w" -o run \
+        -- $B --workload $w --steps 1 --warmup 0 --no-cpu-baseline --no-pmc || exit 1 ;;
+    phase2|phase3)  # per-region wave cycles from the -DRT_PHASES build (cpu-raytracing-rt_amd/ph_build)
+      w=C${s#phase}
+      RT_AMD_LIB=$PWD/cpu-raytracing-rt_amd/ph_build/librt_amd.so run phase_$w 600 \
+        python3 tools/phases.py $w ${PHASE_SPP:-64} || exit 1 ;;
     lane2) run lane_C2 600 python3 tools/lane_util.py C2 256 256 64 32 8 || exit 1 ;;
     lane3) run lane_C3 600 python3 tools/lane_util.py C3 64 64 32 8 || exit 1 ;;
     var2|var3)  # every cpu-raytracing-rt_amd/build*/librt_amd.so variant at reduced spp

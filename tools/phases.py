@@ -1,0 +1,40 @@
+"""Wave-cycle breakdown of the path kernel by code region (needs a -DRT_PHASES
+build: make -C cpu-raytracing-rt_amd/csrc OUT=../ph_build EXTRA=-DRT_PHASES,
+then RT_AMD_LIB=.../ph_build/librt_amd.so).
+usage: python tools/phases.py WORKLOAD [SPP]
+Each region's s_memtime delta is added once per wave that executes it, so the
+shares are of wave-time (all waves summed), the quantity that divergence and
+stalls inflate.  segment = intersect + light sample + light pdf + shading."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402,F401  (one HIP runtime per process)
+import bench  # noqa: E402
+from conftest import load_package  # noqa: E402
+
+NAMES = ["assign", "intersect", "light_sample", "light_pdf", "segment", "commit", "tile",
+         "trav_wave_iters", "trav_lane_iters", "leaf_wave_trips", "leaf_lane_tests"]
+rt = load_package()
+wl = sys.argv[1]
+scene_file, W, H, spp, depth = bench.WORKLOADS[wl]
+if len(sys.argv) > 2:
+    spp = int(sys.argv[2])
+desc, params = bench.load_workload(rt, scene_file, W, H, spp)
+scene = rt.Scene(desc)
+_, _, st = scene.generate_image(params, stats=True)
+raw = scene.read_raw_stats()
+ph = {n: int(raw[16 + i]) for i, n in enumerate(NAMES)}
+tile = max(ph["tile"], 1)
+shading = ph["segment"] - ph["intersect"] - ph["light_sample"] - ph["light_pdf"]
+share = {k: ph[k] / tile for k in ("assign", "intersect", "light_sample", "light_pdf", "commit")}
+share["shading_rest"] = shading / tile
+share["loop_other"] = 1.0 - ph["assign"] / tile - ph["segment"] / tile - ph["commit"] / tile
+print(json.dumps({"workload": wl, "spp": spp, "segments": st["segments"],
+                  "lane_util": st["lane_steps"] / max(1, st["wave_steps"]),
+                  "traversal_loop_util": ph["trav_lane_iters"] / max(1, 64 * ph["trav_wave_iters"]),
+                  "leaf_loop_util": ph["leaf_lane_tests"] / max(1, 64 * ph["leaf_wave_trips"]),
+                  "wave_cycles": ph, "share_of_tile_time": {k: round(v, 4) for k, v in share.items()}}))
