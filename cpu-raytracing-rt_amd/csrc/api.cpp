@@ -81,6 +81,7 @@ int upload_bvh(rt_scene* s, const HostBvhArrays& h, DevBvh& d) {
     store3(d.root_max, h.root.max);
     d.n_prims = h.n_prims;
     d.depth = h.depth;
+    d.fast = h.fast ? 1u : 0u;
     if ((rc = upload(s, h.shapes, &d.shapes))) return rc;
     if ((rc = upload(s, h.tris, &d.tris))) return rc;
     if ((rc = upload(s, h.tri_cold, &d.tri_cold))) return rc;

@@ -127,13 +127,13 @@ RT_D bool shape_closest(const DevShape& s, V3 o, V3 d, const Rcp3& rc, double& t
 }
 
 // BVH::intersection (bvh.rs:27-36) + Node::intersection (bvh.rs:151-186)
-template <int KIND, bool ST>
+template <int KIND, bool ST, bool FAST>
 RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stack& S, Cnt<ST>& C, double& bt_out,
                       double& bu, double& bv, uint32_t& bprim, uint32_t& baux) {
     if (B.n_prims == 0) return false;
     double t0;
     C.aabb();
-    if (!aabb_hit(load3(B.root_min), load3(B.root_max), o, d, rc, t0)) return false;
+    if (!aabb_hit<FAST>(load3(B.root_min), load3(B.root_max), o, d, rc, t0)) return false;
     bool valid = false;
     double best = INFINITY;
     uint32_t node = 0;
@@ -144,7 +144,7 @@ RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stack& S, Cnt
     // the primitive loop runs with many lanes instead of a few.  Each lane's
     // own sequence of visits, tests, `best` updates and pruning is unchanged
     // (the reference's order, bvh.rs:151-210) — only when it runs moves.
-    uint32_t cnt = B.nodes[0].count;
+    uint32_t cnt = B.nodes[0].count, start = B.nodes[0].start;  // current node's primitive range
     bool live = true;
     for (;;) {
         const uint64_t lv = __ballot(live);
@@ -155,7 +155,6 @@ RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stack& S, Cnt
         bool next = false;  // this lane finished its current node and pops
         if (do_leaves) {
             if (live && cnt != 0) {
-                const uint32_t start = B.nodes[node].start;
                 for (uint32_t i = start; i < start + cnt; ++i) {
                     PH_COUNT(kPhLeafWave, kPhLeafLane);
                     double t, u = 0.0, v = 0.0;
@@ -173,22 +172,24 @@ RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stack& S, Cnt
             const DevNode& n = B.nodes[node];
             double lt = 0.0, rt2 = 0.0;
             C.aabb(2);
-            bool lh = aabb_hit(load3(n.lmin), load3(n.lmax), o, d, rc, lt);
-            bool rh = aabb_hit(load3(n.rmin), load3(n.rmax), o, d, rc, rt2);
+            bool lh = aabb_hit<FAST>(load3(n.lmin), load3(n.lmax), o, d, rc, lt);
+            bool rh = aabb_hit<FAST>(load3(n.rmin), load3(n.rmax), o, d, rc, rt2);
             const double bt = best;  // +inf when no hit yet
             const double li = lh ? (lt < bt ? lt : bt) : bt;
             const double ri = rh ? (rt2 < bt ? rt2 : bt) : bt;
             const uint32_t left = (uint32_t)n.left, right = (uint32_t)n.right;
+            bool go_left = false;
             if (li < bt) {
                 if (ri < bt) {
-                    if (li < ri) { S.push(right, ri); node = left; }
-                    else { S.push(left, li); node = right; }
-                } else node = left;
-                cnt = B.nodes[node].count;
-            } else if (ri < bt) {
-                node = right;
-                cnt = B.nodes[node].count;
-            } else next = true;
+                    if (li < ri) { S.push(right, ri); go_left = true; }
+                    else S.push(left, li);
+                } else go_left = true;
+            } else if (!(ri < bt)) next = true;
+            if (!next) {
+                node = go_left ? left : right;
+                cnt = go_left ? n.lcount : n.rcount;
+                start = go_left ? n.lstart : n.rstart;
+            }
         }
         if (next) {  // resume from the stack: far children still closer than best
             bool found = false;
@@ -197,12 +198,21 @@ RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stack& S, Cnt
                 S.pop(nn, tt);
                 if (tt < best) { node = nn; found = true; break; }
             }
-            if (found) cnt = B.nodes[node].count;
+            if (found) { cnt = B.nodes[node].count; start = B.nodes[node].start; }
             else live = false;
         }
     }
     if (valid) bt_out = best;
     return valid;
+}
+
+// Slab tests with the unguarded exact division when the BVH's boxes and this
+// ray allow it (DevBvh::fast, ray_fast); the guarded form otherwise.
+template <int KIND, bool ST>
+RT_D bool bvh_closest_sel(const DevBvh& B, bool rfast, V3 o, V3 d, const Rcp3& rc, Stack& S, Cnt<ST>& C,
+                          double& bt_out, double& bu, double& bv, uint32_t& bprim, uint32_t& baux) {
+    if (B.fast && rfast) return bvh_closest<KIND, ST, true>(B, o, d, rc, S, C, bt_out, bu, bv, bprim, baux);
+    return bvh_closest<KIND, ST, false>(B, o, d, rc, S, C, bt_out, bu, bv, bprim, baux);
 }
 
 // Materialise the winning candidate (model-space normals) + its rotation.
@@ -254,7 +264,8 @@ RT_D bool scene_intersect(const DevScene& S, V3 o, V3 d, Stack& stk, Cnt<ST>& C,
                           int32_t& gid) {
     Cand best;
     best.valid = false; best.t = 0.0; best.u = best.v = 0.0; best.prim = 0; best.aux = 0; best.kind = 0;
-    const Rcp3 rc = make_rcp3(d);  // dead (DCE'd) unless RT_FASTDIV
+    const Rcp3 rc = make_rcp3(d);
+    const bool rfast = ray_fast(o, rc);
     for (uint32_t i = 0; i < S.n_planes; ++i) {  // :45-49
         double t; uint32_t aux;
         C.shape();
@@ -263,19 +274,19 @@ RT_D bool scene_intersect(const DevScene& S, V3 o, V3 d, Stack& stk, Cnt<ST>& C,
     }
     {
         double t, u, v; uint32_t p, aux = 0;
-        if (bvh_closest<1, ST>(S.boxes, o, d, rc, stk, C, t, u, v, p, aux) && (!best.valid || t < best.t)) {
+        if (bvh_closest_sel<1, ST>(S.boxes, rfast, o, d, rc, stk, C, t, u, v, p, aux) && (!best.valid || t < best.t)) {
             best.valid = true; best.t = t; best.prim = p; best.aux = aux; best.kind = 1;
         }
     }
     {
         double t, u, v; uint32_t p, aux = 0;
-        if (bvh_closest<2, ST>(S.ells, o, d, rc, stk, C, t, u, v, p, aux) && (!best.valid || t < best.t)) {
+        if (bvh_closest_sel<2, ST>(S.ells, rfast, o, d, rc, stk, C, t, u, v, p, aux) && (!best.valid || t < best.t)) {
             best.valid = true; best.t = t; best.prim = p; best.aux = aux; best.kind = 2;
         }
     }
     {
         double t, u = 0.0, v = 0.0; uint32_t p, aux = 0;
-        if (bvh_closest<3, ST>(S.tris, o, d, rc, stk, C, t, u, v, p, aux) && (!best.valid || t < best.t)) {
+        if (bvh_closest_sel<3, ST>(S.tris, rfast, o, d, rc, stk, C, t, u, v, p, aux) && (!best.valid || t < best.t)) {
             best.valid = true; best.t = t; best.prim = p; best.u = u; best.v = v; best.aux = 0; best.kind = 3;
         }
     }

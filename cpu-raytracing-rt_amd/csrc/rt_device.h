@@ -153,6 +153,18 @@ RT_D double fdiv_r(double x, double y, double r, bool yok) {
     }
     return x / y;
 }
+// Unguarded form for slab tests whose operands are proven in range up front
+// (scene boxes and ray origin in kCoordLo..kCoordHi or zero, |d| per fd_ok):
+// then x = min - o is 0 or a multiple of 2^-449 below 2^401, so fd_ok(x)
+// always holds except x == +-0, where the result differs from x / y at most in
+// the sign of zero — which no comparison of the slab test observes.
+RT_D double fdiv_fast(double x, double y, double r) {
+    const double q0 = x * r;
+    const double e0 = fma(-q0, y, x);
+    const double q1 = fma(e0, r, q0);
+    const double e1 = fma(-q1, y, x);
+    return fma(e1, r, q1);
+}
 constexpr double kInvPi = 1.0 / kPi;  // RN(1/pi), folded exactly at compile time
 RT_D double div_pi(double x) { return fdiv_r(x, kPi, kInvPi, true); }
 
@@ -164,6 +176,10 @@ struct Rcp3 {
 RT_D Rcp3 make_rcp3(V3 d) {
     return Rcp3{v3(1.0 / d.x, 1.0 / d.y, 1.0 / d.z),
                 (fd_ok(d.x) ? 1u : 0u) | (fd_ok(d.y) ? 2u : 0u) | (fd_ok(d.z) ? 4u : 0u)};
+}
+// a ray whose slab tests may take fdiv_fast (given DevBvh::fast boxes)
+RT_D bool ray_fast(V3 o, const Rcp3& rc) {
+    return rc.ok == 7u && coord_fast(o.x) && coord_fast(o.y) && coord_fast(o.z);
 }
 
 // ------------------------------------------------------------ geometry ----
@@ -178,19 +194,30 @@ RT_D double safe_max(double a, double b) {
     if (!isfinite(b)) return a;
     return rmax(a, b);
 }
+// FAST: the ray passed ray_fast() and the BVH's boxes DevBvh::fast — every
+// slab quotient takes the unguarded exact division (no d == 0 axis either).
+template <bool FAST = false>
 RT_D bool aabb_hit(V3 mn, V3 mx, V3 o, V3 d, const Rcp3& rc, double& t) {
-    if ((d.x == 0.0 && (o.x < mn.x || mx.x < o.x)) || (d.y == 0.0 && (o.y < mn.y || mx.y < o.y)) ||
-        (d.z == 0.0 && (o.z < mn.z || mx.z < o.z)))
+    if (!FAST && ((d.x == 0.0 && (o.x < mn.x || mx.x < o.x)) || (d.y == 0.0 && (o.y < mn.y || mx.y < o.y)) ||
+                  (d.z == 0.0 && (o.z < mn.z || mx.z < o.z))))
         return false;
     if (!(o.x < mn.x || mx.x < o.x || o.y < mn.y || mx.y < o.y || o.z < mn.z || mx.z < o.z)) {
         t = 0.0;  // inside (aabb.rs:58-60)
         return true;
     }
-    const bool okx = rc.ok & 1u, oky = rc.ok & 2u, okz = rc.ok & 4u;
-    V3 tmin = v3(fdiv_r(mn.x - o.x, d.x, rc.r.x, okx), fdiv_r(mn.y - o.y, d.y, rc.r.y, oky),
-                 fdiv_r(mn.z - o.z, d.z, rc.r.z, okz));
-    V3 tmax = v3(fdiv_r(mx.x - o.x, d.x, rc.r.x, okx), fdiv_r(mx.y - o.y, d.y, rc.r.y, oky),
-                 fdiv_r(mx.z - o.z, d.z, rc.r.z, okz));
+    V3 tmin, tmax;
+    if (FAST) {
+        tmin = v3(fdiv_fast(mn.x - o.x, d.x, rc.r.x), fdiv_fast(mn.y - o.y, d.y, rc.r.y),
+                  fdiv_fast(mn.z - o.z, d.z, rc.r.z));
+        tmax = v3(fdiv_fast(mx.x - o.x, d.x, rc.r.x), fdiv_fast(mx.y - o.y, d.y, rc.r.y),
+                  fdiv_fast(mx.z - o.z, d.z, rc.r.z));
+    } else {
+        const bool okx = rc.ok & 1u, oky = rc.ok & 2u, okz = rc.ok & 4u;
+        tmin = v3(fdiv_r(mn.x - o.x, d.x, rc.r.x, okx), fdiv_r(mn.y - o.y, d.y, rc.r.y, oky),
+                  fdiv_r(mn.z - o.z, d.z, rc.r.z, okz));
+        tmax = v3(fdiv_r(mx.x - o.x, d.x, rc.r.x, okx), fdiv_r(mx.y - o.y, d.y, rc.r.y, oky),
+                  fdiv_r(mx.z - o.z, d.z, rc.r.z, okz));
+    }
     double t1x = safe_min(tmin.x, tmax.x), t1y = safe_min(tmin.y, tmax.y), t1z = safe_min(tmin.z, tmax.z);
     double t2x = safe_max(tmin.x, tmax.x), t2y = safe_max(tmin.y, tmax.y), t2z = safe_max(tmin.z, tmax.z);
     double tn = safe_max(safe_max(t1x, t1y), t1z);

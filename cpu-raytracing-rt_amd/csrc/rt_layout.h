@@ -23,6 +23,9 @@ struct alignas(128) DevNode {
     double rmin[3], rmax[3];   // right child's box (bvh.rs:159)
     int32_t left, right;       // child indices, -1 for a leaf
     uint32_t start, count;     // leaf primitive range [start, start+count)
+    // the children's primitive ranges (count 0 = internal child): a descent
+    // learns whether it enters a leaf without loading the child's line
+    uint32_t lstart, lcount, rstart, rcount;
 };
 static_assert(sizeof(DevNode) == 128, "fat node is one 128-B line");
 
@@ -59,6 +62,8 @@ struct DevBvh {
     double root_min[3], root_max[3];
     uint32_t n_prims;
     uint32_t depth;            // levels (root = 1)
+    uint32_t fast;             // every box coordinate is 0 or in [2^-397, 2^400] (coord_fast)
+    uint32_t _pad;
     // primitives in BVH order: exactly one of these is non-null
     const DevShape* shapes;
     const DevTri* tris;

@@ -30,6 +30,12 @@ RT_HD V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
 RT_HD V3 operator-(V3 a) { return v3(-a.x, -a.y, -a.z); }
 RT_HD V3 operator*(V3 a, double s) { return v3(a.x * s, a.y * s, a.z * s); }
 RT_HD V3 operator/(V3 a, double s) { return v3(a.x / s, a.y / s, a.z / s); }
+// Coordinate range of the unguarded exact slab division (rt_device.h fdiv_fast):
+// 0, or 2^-397 <= |v| <= 2^400.
+RT_HD bool coord_fast(double v) {
+    const double a = v < 0.0 ? -v : v;
+    return a == 0.0 || (a >= 0x1p-397 && a <= 0x1p400);
+}
 RT_HD V3 mul(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }   // mul_element_wise
 RT_HD V3 div(V3 a, V3 b) { return v3(a.x / b.x, a.y / b.y, a.z / b.z); }   // div_element_wise
 RT_HD double dot(V3 a, V3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }

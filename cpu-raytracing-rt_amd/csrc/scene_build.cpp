@@ -132,8 +132,12 @@ void flatten(const HostBvh& h, HostBvhArrays& out) {
         d.left = (int32_t)n.left;
         d.right = (int32_t)n.right;
         if (n.left >= 0) {
-            store3(d.lmin, h.nodes[n.left].box.min); store3(d.lmax, h.nodes[n.left].box.max);
-            store3(d.rmin, h.nodes[n.right].box.min); store3(d.rmax, h.nodes[n.right].box.max);
+            const HostNode& l = h.nodes[n.left];
+            const HostNode& r = h.nodes[n.right];
+            store3(d.lmin, l.box.min); store3(d.lmax, l.box.max);
+            store3(d.rmin, r.box.min); store3(d.rmax, r.box.max);
+            d.lstart = (uint32_t)l.start; d.lcount = (uint32_t)(l.end - l.start);
+            d.rstart = (uint32_t)r.start; d.rcount = (uint32_t)(r.end - r.start);
         }
         d.start = (uint32_t)n.start;
         d.count = (uint32_t)(n.end - n.start);
@@ -141,6 +145,12 @@ void flatten(const HostBvh& h, HostBvhArrays& out) {
     }
     out.root = h.nodes.empty() ? box_empty() : h.nodes[0].box;
     out.depth = h.depth;
+    bool fast = !h.nodes.empty();
+    for (const HostNode& n : h.nodes) {
+        const double c[6] = {n.box.min.x, n.box.min.y, n.box.min.z, n.box.max.x, n.box.max.y, n.box.max.z};
+        for (double v : c) fast = fast && coord_fast(v);
+    }
+    out.fast = fast;
 }
 
 struct ShapeItem { DevShape s; uint32_t mat; int32_t gid; Box3 box; };

@@ -42,6 +42,7 @@ struct HostBvhArrays {
     std::vector<DevNode> nodes;
     Box3 root;
     uint32_t n_prims = 0, depth = 0;
+    bool fast = false;  // all box coordinates pass coord_fast (DevBvh::fast)
     std::vector<DevShape> shapes;
     std::vector<DevTri> tris;
     std::vector<DevTriCold> tri_cold;

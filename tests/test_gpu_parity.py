@@ -127,6 +127,45 @@ def test_intersect_rays_random(sink, rt):
     assert np.array_equal(gh.view(np.uint8), oh.view(np.uint8))
 
 
+def _tri_soup(rt, scale, n=400, seed=0):
+    """Smooth-normal triangle soup (tri_mode GLTF) scaled by `scale`; every 7th is emissive."""
+    rng = np.random.default_rng(seed)
+    v = rng.uniform(-1, 1, (n, 1, 3)) + 0.25 * rng.standard_normal((n, 3, 3))
+    nrm = rng.standard_normal((n, 3, 3))
+    nrm /= np.linalg.norm(nrm, axis=2, keepdims=True)
+    mats = np.zeros(2, rt.MATERIAL_DTYPE)
+    mats[0]["color"] = [0.6, 0.6, 0.6]
+    mats[1]["color"] = [1.0, 1.0, 1.0]
+    mats[1]["emission"] = [2.0, 2.0, 2.0]
+    return rt.SceneDesc(materials=mats, shapes=np.zeros(0, rt.SHAPE_DTYPE),
+                        tri_vertices=(v * scale).reshape(n, 9), tri_normals=nrm.reshape(n, 9),
+                        tri_material=(np.arange(n) % 7 == 0).astype(np.uint32), tri_mode=rt.RT_TRI_GLTF)
+
+
+@pytest.mark.parametrize("scale", [1.0, 2.0 ** 420, 2.0 ** -420])
+def test_slab_division_paths(rt, orc, scale):
+    """Boxes inside the fdiv_fast range (scale 1) and outside it (2^+-420: guarded
+    division everywhere) give the oracle's hits and light pdfs bit for bit."""
+    desc = _tri_soup(rt, scale)
+    g, o = rt.Scene(desc), orc.OracleScene(desc)
+    rng = np.random.default_rng(8)
+    n = 30000
+    orig = rng.uniform(-1.5, 1.5, (n, 3)) * scale
+    d = rng.standard_normal((n, 3))
+    d[:50, 1] = 0.0          # axis-parallel rays: d == 0 slabs
+    d[50:60] = [1e-200, 1.0, 0.5]  # a direction component below the fast range
+    rays = np.concatenate([orig, d], axis=1)
+    gh, oh = g.intersect(rays), o.intersect(rays)
+    assert np.array_equal(gh.view(np.uint8), oh.view(np.uint8))
+    if scale >= 1.0:  # at 2^-420 the determinant epsilon rejects every triangle, as in the reference
+        assert (gh["prim"] >= 0).sum() > 1000
+    dn = d / np.linalg.norm(d, axis=1, keepdims=True)
+    pd = np.concatenate([orig, dn], axis=1)
+    # at 2^420 the light areas overflow and Light::pdf is NaN, as in the
+    # reference: NaNs must sit in the same places, everything else bit-equal
+    assert np.array_equal(g.light_pdf(pd), o.light_pdf(pd), equal_nan=True)
+
+
 def test_light_pdf_random(sink):
     desc, params, g, o = sink
     rng = np.random.default_rng(4)
