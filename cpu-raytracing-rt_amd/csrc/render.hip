@@ -3,10 +3,11 @@
 //   path_kernel          generate_image pixel loop (main.rs:94-103) fused with
 //                        Camera::fuzzy_ray (camera.rs:48-55) and raytrace /
 //                        raytrace_impl (raytrace.rs:8-60) in throughput form.
-//                        One lane = one pixel; the lane walks its spp samples
-//                        in order (deterministic per-pixel sum) and regenerates
-//                        a camera path as soon as one ends, so lanes whose paths
-//                        are short do not idle while a neighbour finishes.
+//                        Persistent 64-lane waves pull (tile, sample chunk,
+//                        quadrant) wave-tiles from a queue; inside one, lanes
+//                        take (sample, pixel) paths dynamically and commit
+//                        radiance per pixel in sample order.
+//   reduce_chunks_kernel chunk partial sums -> per-pixel mean
 //   intersect_kernel     batch `intersect` (intersections.rs:42-62)
 //   light_kernel         batch intersect_lights / Light::pdf
 //                        (intersections.rs:87-91, ray_sampler.rs:132-139)
