@@ -1,0 +1,51 @@
+// phases.h — diagnostics of the path kernel (tools/phases.py); compiled in only
+// with -DRT_PHASES, so product builds carry none of it.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace rt {
+
+// ---- diagnostics: wave cycles per code region (tools/phases.py) ----------
+// Only in -DRT_PHASES builds: s_memtime deltas, added once per wave by the
+// first active lane into LDS, flushed to raw stats words 16..23 (kPhase*).
+// The last four words count BVH traversal-loop iterations (wave-level and
+// summed over lanes) and primitive tests (wave-level inner-loop trips and
+// lane-level tests): their ratios are the loop's SIMD utilisation.
+// Regions timed with PH_ADDW also add cycles x (active lanes / 64) at k + kPhW:
+// the ratio of the two is the region's lane utilisation.
+enum { kPhAssign, kPhIntersect, kPhLightSample, kPhLightPdf, kPhSegment, kPhCommit, kPhTile,
+       kPhTravWave, kPhTravLane, kPhLeafWave, kPhLeafLane, kPhRngWave, kPhRngLane, kPhW0,
+       kPhN = kPhW0 + 5 };
+constexpr int kPhW = kPhW0 - kPhIntersect;  // weighted word of region k = k + kPhW (k in 1..5)
+#ifdef RT_PHASES
+__shared__ unsigned long long g_phase[kPhN];
+#define PH_T() __builtin_amdgcn_s_memtime()
+#define PH_FIRST() (__lane_id() == (unsigned)__builtin_amdgcn_readfirstlane(__lane_id()))
+// (atomics, so the compiler cannot keep a lane-private copy across iterations)
+#define PH_ADD(k, t0)                                                                        \
+    do {                                                                                     \
+        const unsigned long long dt_ = PH_T() - (t0);                                        \
+        if (PH_FIRST()) atomicAdd(&g_phase[k], dt_);                                         \
+    } while (0)
+#define PH_COUNT(kw, kl)                                                                     \
+    do {                                                                                     \
+        if (PH_FIRST()) atomicAdd(&g_phase[kw], 1ull);                                       \
+        atomicAdd(&g_phase[kl], 1ull);                                                       \
+    } while (0)
+#define PH_ADDW(k, t0)                                                                       \
+    do {                                                                                     \
+        const unsigned long long dt_ = PH_T() - (t0);                                        \
+        const unsigned long long act_ = (unsigned long long)__popcll(__ballot(1));           \
+        if (PH_FIRST()) {                                                                    \
+            atomicAdd(&g_phase[k], dt_);                                                     \
+            atomicAdd(&g_phase[(k) + kPhW], dt_ * act_ / 64ull);                             \
+        }                                                                                    \
+    } while (0)
+#else
+#define PH_T() 0ull
+#define PH_ADD(k, t0) ((void)(t0))
+#define PH_ADDW(k, t0) ((void)(t0))
+#define PH_COUNT(kw, kl) ((void)0)
+#endif
+
+}  // namespace rt

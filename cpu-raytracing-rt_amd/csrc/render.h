@@ -31,8 +31,8 @@ struct KParams {
 // device work counters: paths, segments, aabb, tri, shape, shaded, light queries,
 // light hits, lane steps, wave steps (64 x longest lane) — rt_stats order
 constexpr int kNStats = 10;
-constexpr int kStatsWords = 32;   // device counter words (rt_read_raw_stats)
-constexpr int kPhaseWord0 = 16;   // RT_PHASES builds: region cycles + loop counts at words 16..26
+constexpr int kStatsWords = 48;   // device counter words (rt_read_raw_stats)
+constexpr int kPhaseWord0 = 16;   // RT_PHASES builds: region cycles + loop counts at words 16..33
 
 // Chunk count for a frame: a function of (W, H, spp) only, so the image does not
 // depend on the number of GPUs.  Doubles while the frame has < kChunkLanes

@@ -39,34 +39,6 @@ constexpr int kLeafBatch = RT_LEAF_BATCH;
 // hit consecutive banks for any block size.
 constexpr int kWave = 64;
 
-// ---- diagnostics: wave cycles per code region (tools/phases.py) ----------
-// Only in -DRT_PHASES builds: s_memtime deltas, added once per wave by the
-// first active lane into LDS, flushed to raw stats words 16..23 (kPhase*).
-// The last four words count BVH traversal-loop iterations (wave-level and
-// summed over lanes) and primitive tests (wave-level inner-loop trips and
-// lane-level tests): their ratios are the loop's SIMD utilisation.
-enum { kPhAssign, kPhIntersect, kPhLightSample, kPhLightPdf, kPhSegment, kPhCommit, kPhTile,
-       kPhTravWave, kPhTravLane, kPhLeafWave, kPhLeafLane, kPhN };
-#ifdef RT_PHASES
-__shared__ unsigned long long g_phase[kPhN];
-#define PH_T() __builtin_amdgcn_s_memtime()
-#define PH_FIRST() (__lane_id() == (unsigned)__builtin_amdgcn_readfirstlane(__lane_id()))
-// (atomics, so the compiler cannot keep a lane-private copy across iterations)
-#define PH_ADD(k, t0)                                                                        \
-    do {                                                                                     \
-        const unsigned long long dt_ = PH_T() - (t0);                                        \
-        if (PH_FIRST()) atomicAdd(&g_phase[k], dt_);                                         \
-    } while (0)
-#define PH_COUNT(kw, kl)                                                                     \
-    do {                                                                                     \
-        if (PH_FIRST()) atomicAdd(&g_phase[kw], 1ull);                                       \
-        atomicAdd(&g_phase[kl], 1ull);                                                       \
-    } while (0)
-#else
-#define PH_T() 0ull
-#define PH_ADD(k, t0) ((void)(t0))
-#define PH_COUNT(kw, kl) ((void)0)
-#endif
 struct Stack {
     uint32_t* sn;        // LDS node slots, stride kWave
     double* st;          // LDS entry-t slots, stride kWave
@@ -408,7 +380,9 @@ RT_D double light_pdf(const DevScene& S, V3 pos, V3 dir, Stack& stk, Cnt<ST>& C)
 
 // ------------------------------------------------------------ samplers ----
 RT_D V3 uniform_on_sphere(Rng& r) {  // ray_sampler.rs:159-170
-    double a0 = gen_f64(r), a1 = gen_f64(r), a2 = gen_f64(r);
+    double a0 = gen_f64(r);
+    rng_top_up(r);  // 6 words here may exceed current + next (see Rng)
+    double a1 = gen_f64(r), a2 = gen_f64(r);
     return normalize(v3(a0 * 2.0 - 1.0, a1 * 2.0 - 1.0, a2 * 2.0 - 1.0));
 }
 RT_D V3 cosine_sample(V3 n, Rng& r) {  // ray_sampler.rs:69-76
@@ -427,6 +401,7 @@ RT_D V3 uniform_on_box(V3 s, Rng& r, const Scales& sc) {  // ray_sampler.rs:142-
     double w4x = s.y * s.z, w4y = s.x * s.z, w4z = s.x * s.y;
     double choice = gen_range(r, 0.0, (w4x + w4y) + w4z);
     double sign = (double)(gen_sign_bit(r) * 2 - 1);
+    rng_top_up(r);
     double u1 = gen_range_incl(r, -1.0, sc.s11);
     double u2 = gen_range_incl(r, -1.0, sc.s11);
     V3 p;
@@ -437,6 +412,7 @@ RT_D V3 uniform_on_box(V3 s, Rng& r, const Scales& sc) {  // ray_sampler.rs:142-
 }
 RT_D V3 light_sample(const DevScene& S, V3 pos, Rng& r, const Scales& sc) {  // ray_sampler.rs:101-130
     uint64_t index = gen_index(r, S.n_lights);
+    rng_top_up(r);
     const uint32_t nb = S.lboxes.n_prims, ne = S.lells.n_prims;
     V3 world;
     if (index < nb) {
@@ -475,13 +451,14 @@ RT_D bool segment(const DevScene& S, const KParams& P, const Scales& sc, PathSta
     C.segment();
     const unsigned long long ph0 = PH_T();
     const bool hit = scene_intersect<ST>(S, ps.o, ps.d, stk, C, h, mat, gid);
-    PH_ADD(kPhIntersect, ph0);
+    PH_ADDW(kPhIntersect, ph0);
     if (!hit) {
         hit_gid = RT_HIT_MISS;
         ps.L = ps.L + mul(ps.T, load3(P.bg));
         return false;
     }
     hit_gid = gid;
+    rng_top_up(rng);  // every hit lane here: a coherent refill point
     const DevMaterial& m = S.mats[mat];
     const V3 col = load3(m.color);
     ps.L = ps.L + mul(ps.T, load3(m.emission));
@@ -490,11 +467,13 @@ RT_D bool segment(const DevScene& S, const KParams& P, const Scales& sc, PathSta
         V3 pos = o + d * h.t;
         const bool empty = S.n_lights == 0;
         V3 dir;
-        if (empty || gen_bool(rng, 0.5)) dir = cosine_sample(h.ns, rng);   // Mix::sample (ray_sampler.rs:87-93)
+        const bool by_cosine = empty || gen_bool(rng, 0.5);  // Mix::sample (ray_sampler.rs:87-93)
+        rng_top_up(rng);
+        if (by_cosine) dir = cosine_sample(h.ns, rng);
         else {
             const unsigned long long ph1 = PH_T();
             dir = light_sample(S, pos, rng, sc);
-            PH_ADD(kPhLightSample, ph1);
+            PH_ADDW(kPhLightSample, ph1);
         }
         const double cs = dot(dir, h.ns);
         if (cs <= 0.0) return false;
@@ -502,7 +481,7 @@ RT_D bool segment(const DevScene& S, const KParams& P, const Scales& sc, PathSta
         if (!empty) {
             const unsigned long long ph2 = PH_T();
             lp = light_pdf<ST>(S, pos, dir, stk, C);
-            PH_ADD(kPhLightPdf, ph2);
+            PH_ADDW(kPhLightPdf, ph2);
         }
         double pdf = empty ? cosine_pdf(h.ns, dir) : (cosine_pdf(h.ns, dir) + lp) / 2.0;  // Mix::pdf
         if (pdf == 0.0) return false;
@@ -646,6 +625,7 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene S, KParams 
                         // Camera::fuzzy_ray + raytrace (camera.rs:48-55, raytrace.rs:8-10)
                         pixel = (uint64_t)py * P.width + px;
                         rng_init(rng, P.seed, pixel, s);
+                        rng_top_up(rng);
                         const double fx = (double)px + gen_range(rng, 0.0, 1.0);
                         const double fy = (double)py + gen_range(rng, 0.0, 1.0);
                         const double x = (2.0 * fx / P.fw - 1.0) * P.tan_x;
@@ -673,7 +653,7 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene S, KParams 
                     int32_t g;
                     const unsigned long long ph_s = PH_T();
                     cont = segment<ST>(S, P, sc, ps, rng, stk, C, g);
-                    PH_ADD(kPhSegment, ph_s);
+                    PH_ADDW(kPhSegment, ph_s);
                     if (HIT) hit_ids[(pixel * P.spp + s) * depth + b] = g;
                     ++b;
                 }

@@ -8,6 +8,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "phases.h"
 #include "rt_layout.h"
 #include "rt_math.h"
 
@@ -21,11 +22,21 @@ namespace rt {
 // Words are consumed in order; next_u64 = lo word | hi word << 32 (rand
 // BlockRng order).  The 4-word block lives in two u64 "queues" so no
 // dynamically indexed register array (which would go to scratch).
+//
+// Refills are where divergence bites: lanes sit at different offsets of their
+// block, so a refill inside every draw would run Philox at nearly every call
+// site for a handful of lanes.  So the NEXT block is generated ahead at a few
+// coherent points (rng_top_up: path start, each hit, before the diffuse
+// sampler) and a draw that empties the current block only swaps it in.  The
+// word stream is unchanged — blocks are still produced and consumed in counter
+// order; only when they are computed moves.
 struct Rng {
     uint32_t sample, pix_lo, pix_hi, k0, k1;
-    uint32_t blk;       // next block counter
-    uint32_t avail;     // words left in q0/q1
-    uint64_t q0, q1;
+    uint32_t blk;       // counter of the next block to generate
+    uint32_t avail;     // words left in q0/q1 (current block)
+    uint32_t nready;    // n0/n1 holds block blk-1, not yet current
+    uint64_t q0, q1;    // current block
+    uint64_t n0, n1;    // next block
 };
 
 RT_D void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
@@ -33,8 +44,10 @@ RT_D void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
         if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
-        uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-        uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        // one 32x32->64 product per multiplier (v_mad_u64_u32) instead of mul_hi + mul_lo
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
         uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
         c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
     }
@@ -44,12 +57,28 @@ RT_D void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0
 RT_D void rng_init(Rng& r, uint64_t seed, uint64_t pixel, uint32_t sample) {
     r.sample = sample; r.pix_lo = (uint32_t)pixel; r.pix_hi = (uint32_t)(pixel >> 32);
     r.k0 = (uint32_t)seed; r.k1 = (uint32_t)(seed >> 32);
-    r.blk = 0; r.avail = 0; r.q0 = 0; r.q1 = 0;
+    r.blk = 0; r.avail = 0; r.nready = 0; r.q0 = r.q1 = r.n0 = r.n1 = 0;
+}
+// Fallback for the rare draw that finds no next block ready.
+RT_D void philox_next(Rng& r) {
+    PH_COUNT(kPhRngWave, kPhRngLane);
+    philox(r.blk, r.sample, r.pix_lo, r.pix_hi, r.k0, r.k1, r.n0, r.n1);
+    r.blk++;
+    r.nready = 1;
+}
+RT_D void rng_top_up(Rng& r) {  // coherent refill point (see Rng)
+    if (!r.nready) {
+        PH_COUNT(kPhRngWave, kPhRngLane);
+        philox(r.blk, r.sample, r.pix_lo, r.pix_hi, r.k0, r.k1, r.n0, r.n1);
+        r.blk++;
+        r.nready = 1;
+    }
 }
 RT_D uint32_t next_u32(Rng& r) {
     if (r.avail == 0) {
-        philox(r.blk, r.sample, r.pix_lo, r.pix_hi, r.k0, r.k1, r.q0, r.q1);
-        r.blk++;
+        if (!r.nready) philox_next(r);
+        r.q0 = r.n0; r.q1 = r.n1;
+        r.nready = 0;
         r.avail = 4;
     }
     uint32_t w = (uint32_t)r.q0;

@@ -17,7 +17,9 @@ import bench  # noqa: E402
 from conftest import load_package  # noqa: E402
 
 NAMES = ["assign", "intersect", "light_sample", "light_pdf", "segment", "commit", "tile",
-         "trav_wave_iters", "trav_lane_iters", "leaf_wave_trips", "leaf_lane_tests"]
+         "trav_wave_iters", "trav_lane_iters", "leaf_wave_trips", "leaf_lane_tests",
+         "rng_wave_refills", "rng_lane_refills",
+         "w_intersect", "w_light_sample", "w_light_pdf", "w_segment", "w_commit"]
 rt = load_package()
 wl = sys.argv[1]
 scene_file, W, H, spp, depth = bench.WORKLOADS[wl]
@@ -26,7 +28,7 @@ if len(sys.argv) > 2:
 desc, params = bench.load_workload(rt, scene_file, W, H, spp)
 scene = rt.Scene(desc)
 _, _, st = scene.generate_image(params, stats=True)
-raw = scene.read_raw_stats()
+raw = scene.read_raw_stats(48)
 ph = {n: int(raw[16 + i]) for i, n in enumerate(NAMES)}
 tile = max(ph["tile"], 1)
 shading = ph["segment"] - ph["intersect"] - ph["light_sample"] - ph["light_pdf"]
@@ -37,4 +39,8 @@ print(json.dumps({"workload": wl, "spp": spp, "segments": st["segments"],
                   "lane_util": st["lane_steps"] / max(1, st["wave_steps"]),
                   "traversal_loop_util": ph["trav_lane_iters"] / max(1, 64 * ph["trav_wave_iters"]),
                   "leaf_loop_util": ph["leaf_lane_tests"] / max(1, 64 * ph["leaf_wave_trips"]),
+                  "rng_refill_util": ph["rng_lane_refills"] / max(1, 64 * ph["rng_wave_refills"]),
+                  "rng_wave_refills_per_segment": ph["rng_wave_refills"] * 64 / max(1, st["segments"]),
+                  "region_entry_lane_util": {k: round(ph["w_" + k] / max(1, ph[k]), 4)
+                                             for k in ("intersect", "light_sample", "light_pdf", "segment")},
                   "wave_cycles": ph, "share_of_tile_time": {k: round(v, 4) for k, v in share.items()}}))
