@@ -56,6 +56,9 @@ struct rt_scene {
     double* ring = nullptr;
     size_t ring_entries = 0;
     unsigned long long* d_stats = nullptr;
+    // the path kernel reads the scene record and the frame constants by pointer
+    DevScene* d_scene = nullptr;
+    KParams* d_params = nullptr;
 };
 
 namespace {
@@ -103,6 +106,8 @@ void free_scene(rt_scene* s) {
     if (s->queue) (void)hipFree(s->queue);
     if (s->ring) (void)hipFree(s->ring);
     if (s->d_stats) (void)hipFree(s->d_stats);
+    if (s->d_scene) (void)hipFree(s->d_scene);
+    if (s->d_params) (void)hipFree(s->d_params);
     (void)hipSetDevice(cur);
     delete s;
 }
@@ -224,6 +229,7 @@ int prepare_path(rt_scene* s, const KParams& k, bool stats, bool hits, PathWork&
         s->ring_entries = ring_need;
     }
     W.queue = s->queue; W.ring = s->ring; W.part = s->part;
+    W.d_scene = s->d_scene; W.d_params = s->d_params;
     W.spill_n = s->spill_n; W.spill_t = s->spill_t;
     return RT_OK;
 }
@@ -288,6 +294,9 @@ int rt_scene_create(const rt_scene_desc* desc, rt_scene** out) {
         s->info.bvh_nodes[k] = hs.bvh[k].nodes.size();
         s->info.bvh_depth[k] = hs.bvh[k].depth;
     }
+    HIP_TRY(hipMalloc(&s->d_scene, sizeof(DevScene)));
+    HIP_TRY(hipMemcpy(s->d_scene, &s->dev, sizeof(DevScene), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&s->d_params, sizeof(KParams)));
     HIP_TRY(hipMalloc(&s->d_stats, kStatsWords * sizeof(unsigned long long)));
     HIP_TRY(hipMemset(s->d_stats, 0, kStatsWords * sizeof(unsigned long long)));
     s->info.n_planes = d.n_planes;

@@ -49,6 +49,8 @@ inline void sample_chunks(uint32_t W, uint32_t H, uint32_t spp, uint32_t& chunks
 
 // Device workspace of one path-kernel launch (owned by the scene).
 struct PathWork {
+    const DevScene* d_scene;  // the scene record in device memory (uploaded once)
+    KParams* d_params;        // frame constants slot, staged by launch_path
     uint32_t waves;       // register budget of the kernel instance: 3 or 4 waves/SIMD
     uint32_t grid;        // persistent waves (path_grid)
     uint32_t* queue;      // wave-tile counter, zeroed by launch_path

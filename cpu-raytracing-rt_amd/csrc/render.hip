@@ -563,8 +563,21 @@ constexpr int kRing = (int)kRingRows;
 
 // WAVES = minimum waves per SIMD the register budget must allow (3: 168 VGPRs,
 // 4: 128 VGPRs + spill); chosen per scene by the host.
+//
+// The scene and frame constants come by pointer (device memory), and each loop
+// trip re-derives the pointers through opaque(): their fields are then
+// scalar-loaded where used instead of being hoisted into SGPRs for the whole
+// kernel, which (with ~1 KB of them) spilled hundreds of SGPRs into VGPR lanes.
+template <class T>
+RT_D const T* opaque(const T* p) {
+    asm volatile("" : "+s"(p));
+    return p;
+}
+
 template <bool ST, bool HIT, int WAVES>
-__global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene S, KParams P, double* __restrict__ out,
+__global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams Pv,
+                                                     const DevScene* __restrict__ Sg,
+                                                     const KParams* __restrict__ Pg, double* __restrict__ out,
                                                      double* __restrict__ part, int32_t* __restrict__ hit_ids,
                                                      unsigned long long* __restrict__ stats, uint32_t* spill_n,
                                                      double* spill_t, uint32_t* __restrict__ queue,
@@ -576,9 +589,9 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene S, KParams 
     Stack stk = make_stack(s_n, s_t, lane, (uint64_t)blockIdx.x * kWave + lane, spill_n, spill_t,
                            gridDim.x * kWave);
     double* ring = ring_all + (uint64_t)blockIdx.x * kRing * kWave * 3;
-    const Scales sc{P.scale01, P.scale11};
-    const uint32_t depth = P.ray_depth;
-    const uint32_t n_units = P.n_slots * P.chunks * 4u;
+    const KParams& Pt = WAVES == 3 ? *Pg : Pv;  // per-wave-tile constants
+    const uint32_t depth = Pt.ray_depth;
+    const uint32_t n_units = Pt.n_slots * Pt.chunks * 4u;
     const uint64_t below = (1ull << lane) - 1ull;
     Cnt<ST> C;
     C.zero();
@@ -593,13 +606,13 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene S, KParams 
         const uint32_t unit = __builtin_amdgcn_readfirstlane(u);
         if (unit >= n_units) break;
         const uint32_t quad = unit & 3u, sci = unit >> 2;  // sci = slot * chunks + chunk
-        const uint32_t slot = sci / P.chunks, chunk = sci % P.chunks;
-        const uint64_t tile = (uint64_t)P.rank + (uint64_t)slot * P.world;
-        const bool tile_ok = tile < P.n_tiles;
-        const uint32_t qx0 = (uint32_t)(tile % P.tiles_x) * RT_TILE + (quad & 1u) * 8u;
-        const uint32_t qy0 = (uint32_t)(tile / P.tiles_x) * RT_TILE + (quad >> 1) * 8u;
-        const uint32_t s0 = chunk * P.chunk_spp;
-        const uint32_t nrows = min(P.spp, s0 + P.chunk_spp) - s0, total = nrows * kWave;
+        const uint32_t slot = sci / Pt.chunks, chunk = sci % Pt.chunks;
+        const uint64_t tile = (uint64_t)Pt.rank + (uint64_t)slot * Pt.world;
+        const bool tile_ok = tile < Pt.n_tiles;
+        const uint32_t qx0 = (uint32_t)(tile % Pt.tiles_x) * RT_TILE + (quad & 1u) * 8u;
+        const uint32_t qy0 = (uint32_t)(tile / Pt.tiles_x) * RT_TILE + (quad >> 1) * 8u;
+        const uint32_t s0 = chunk * Pt.chunk_spp;
+        const uint32_t nrows = min(Pt.spp, s0 + Pt.chunk_spp) - s0, total = nrows * kWave;
         if (lane < kRing) s_cnt[lane] = 0;
         __syncthreads();
         V3 sum = v3(0.0, 0.0, 0.0);
@@ -610,6 +623,12 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene S, KParams 
         PathState ps;
         Rng rng;
         for (;;) {
+            // 3 waves: fields scalar-loaded where used (see opaque).  4 waves: the
+            // by-value kernel arguments, which measured faster at its 128-VGPR
+            // budget (C3 2024 vs 2067 ms)
+            const DevScene& S = WAVES == 3 ? *opaque(Sg) : Sv;
+            const KParams& P = WAVES == 3 ? *opaque(Pg) : Pv;
+            const Scales sc{P.scale01, P.scale11};
             // hand the next units to idle lanes, in lane order, inside the ring window
             const uint32_t limit = min(total, (base + kRing) * kWave);
             const uint64_t idle = __ballot(!busy);
@@ -682,9 +701,9 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene S, KParams 
             if (base >= nrows) break;
         }
         const uint32_t lx = (quad & 1u) * 8u + (lane & 7u), ly = (quad >> 1) * 8u + (lane >> 3);
-        const bool own = tile_ok && qx0 + (lane & 7u) < P.width && qy0 + (lane >> 3) < P.height;
-        V3 res = own ? (P.chunks == 1 ? sum / (double)P.spp : sum) : v3(0.0, 0.0, 0.0);  // main.rs:104
-        double* o = P.chunks == 1 ? out + ((uint64_t)slot * kBlock + ly * RT_TILE + lx) * 3
+        const bool own = tile_ok && qx0 + (lane & 7u) < Pt.width && qy0 + (lane >> 3) < Pt.height;
+        V3 res = own ? (Pt.chunks == 1 ? sum / (double)Pt.spp : sum) : v3(0.0, 0.0, 0.0);  // main.rs:104
+        double* o = Pt.chunks == 1 ? out + ((uint64_t)slot * kBlock + ly * RT_TILE + lx) * 3
                                   : part + ((uint64_t)sci * kBlock + ly * RT_TILE + lx) * 3;
         o[0] = res.x; o[1] = res.y; o[2] = res.z;
         wave_flush<ST>(C, stats, witers);
@@ -759,8 +778,8 @@ __global__ void fp64_probe_kernel(const double* a, const double* b, double* out,
 // once (occupancy x CUs), capped by the number of wave-tiles.  Extra waves
 // would only find the queue drained.
 namespace {
-using PathFn = void (*)(DevScene, KParams, double*, double*, int32_t*, unsigned long long*, uint32_t*, double*,
-                        uint32_t*, double*);
+using PathFn = void (*)(DevScene, KParams, const DevScene*, const KParams*, double*, double*, int32_t*,
+                        unsigned long long*, uint32_t*, double*, uint32_t*, double*);
 PathFn path_fn(bool stats, bool hits, uint32_t waves) {
     static const PathFn tab[8] = {path_kernel<false, false, 3>, path_kernel<false, false, 4>,
                                   path_kernel<false, true, 3>,  path_kernel<false, true, 4>,
@@ -782,14 +801,21 @@ hipError_t path_grid(bool stats, bool hits, uint32_t waves, uint32_t n_units, ui
     return hipSuccess;
 }
 
+__global__ void stage_params_kernel(KParams* dst, KParams P) { *dst = P; }
+
 hipError_t launch_path(const DevScene& S, const KParams& P, const PathWork& W, double* out, int32_t* hit_ids,
                        unsigned long long* stats, hipStream_t st) {
     if (P.chunks == 0 || (P.chunks > 1 && !W.part) || !W.queue || !W.ring || W.grid == 0) return hipErrorInvalidValue;
     if (W.waves != 3 && W.waves != 4) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(W.queue, 0, kQueueWords * sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(path_fn(stats != nullptr, hit_ids != nullptr, W.waves), dim3(W.grid), dim3(kWave), 0, st, S,
-                       P, out, W.part, hit_ids, stats, W.spill_n, W.spill_t, W.queue, W.ring);
+    // the frame constants travel by pointer (see opaque): stage them in the scene's
+    // slot, stream-ordered (the by-value argument is captured at launch)
+    hipLaunchKernelGGL(stage_params_kernel, dim3(1), dim3(1), 0, st, W.d_params, P);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(path_fn(stats != nullptr, hit_ids != nullptr, W.waves), dim3(W.grid), dim3(kWave), 0, st,
+                       S, P, W.d_scene, W.d_params, out, W.part, hit_ids, stats, W.spill_n, W.spill_t, W.queue, W.ring);
     e = hipGetLastError();
     if (e != hipSuccess || P.chunks == 1) return e;
     return launch_reduce_chunks(W.part, out, P, st);
