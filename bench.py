@@ -69,7 +69,7 @@ def algo_bytes(st):
     return B_AABB * st["aabb_tests"] + B_TRI * st["tri_tests"] + B_SHAPE * st["shape_tests"] + B_SHADE * st["shaded_hits"]
 
 
-PATH_KERNEL = "path_kernel<false, false>"
+PATH_KERNEL = "path_kernel<false, false,"  # the timed instance (any waves/SIMD budget)
 
 
 def pmc_traffic(args):
@@ -256,7 +256,7 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "traffic_detail": traffic_detail,
-                "kernel": "rt::path_kernel<false,false>",
+                "kernel": "rt::path_kernel<false,false,W> (W = waves/SIMD budget chosen for the scene)",
                 "kernel_ms": kern_ms,
                 "algorithmic_bytes_per_launch": algo_bytes(st),
                 "bytes_model": "32*aabb_tests + 72*tri_tests + 80*shape_tests + 100*shaded_hits (rank 0 tiles)",
