@@ -12,8 +12,10 @@
 #include "scene_build.h"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstring>
+#include <thread>
 
 namespace rt {
 
@@ -55,6 +57,8 @@ Box3 rotated_box(const Box3& b, Quat r) {  // scene.rs:255-268
     return o;
 }
 
+constexpr uint64_t kParallelBuildMin = 200000;  // primitives: below this one thread builds
+
 inline int64_t total_key(double x) {  // f64::total_cmp as an integer key
     int64_t b;
     std::memcpy(&b, &x, 8);
@@ -66,59 +70,153 @@ inline double score(const Box3& b) {  // bvh.rs:115-118
     return s.x * s.y + s.x * s.z + s.y * s.z;
 }
 
+// build_nodes (bvh.rs:75-113) in O(n log n) with the identical result.
+//
+// The reference re-sorts every node's primitives by midpoint on each axis
+// (bvh.rs:102,121, here with ties by list index: a total order).  A total order
+// restricted to a subset is the subset's sorted order, so each axis is sorted
+// ONCE (S[a]) and a split stably partitions the other two axes' lists: every
+// node then sees exactly the sequences the reference sorts, the SAH sweeps run
+// the same float operations in the same order (same strict-< first minimum),
+// nodes are numbered in the same pre-order, and leaves keep the reference's
+// primitive order — the parent's split-axis order for n <= 4 (the root: list
+// order), the axis-2 order (the last sort) for a SameNode leaf.
 struct Builder {
     const std::vector<Box3>& boxes;
-    std::vector<int64_t> key[3];       // midpoint sort key per axis and primitive
-    std::vector<uint64_t>& idx;
-    std::vector<HostNode>& nodes;
-    std::vector<Box3> fwd, bwd;
-    uint32_t depth = 0;
+    std::vector<int64_t> key[3];   // midpoint sort key per axis and primitive
+    // positions lo..hi of a node hold its primitives sorted on each axis (S) and
+    // their boxes in the same order (SB, so sweeps stream instead of gathering)
+    std::vector<uint64_t> S[3];
+    std::vector<Box3> SB[3];
+    std::vector<uint64_t>& order;  // output: leaf primitives, leaf ranges as in the reference
+    // scratch indexed by position (disjoint per node, so subtrees build concurrently)
+    std::vector<double> bwd_score;
+    std::vector<uint8_t> left_flag;  // indexed by primitive id (disjoint per node)
+    std::vector<uint64_t> tmp_i;
+    std::vector<Box3> tmp_b;
 
-    void sort_axis(uint64_t lo, uint64_t hi, int axis) {  // midpoint_comparator (bvh.rs:137-140)
-        const std::vector<int64_t>& k = key[axis];
-        std::sort(idx.begin() + lo, idx.begin() + hi, [&k](uint64_t a, uint64_t b) {
-            return k[a] != k[b] ? k[a] < k[b] : a < b;
-        });
+    struct Out {  // nodes of one (sub)tree in local pre-order
+        std::vector<HostNode> nodes;
+        uint32_t depth = 0;
+    };
+    struct Job { uint64_t lo, hi; uint32_t level; int parent_axis; Out out; };
+    std::vector<Job> jobs;
+    uint32_t par_level = 0;     // 0: build everything in the calling thread
+    uint64_t par_min = 0;       // a subtree smaller than this is never split off
+
+    void presort() {
+        const uint64_t n = boxes.size();
+        std::vector<std::thread> th;
+        for (int a = 0; a < 3; ++a) {
+            th.emplace_back([this, a, n] {  // midpoint_comparator (bvh.rs:137-140), ties by index
+                S[a].resize(n);
+                for (uint64_t i = 0; i < n; ++i) S[a][i] = i;
+                const std::vector<int64_t>& k = key[a];
+                std::sort(S[a].begin(), S[a].end(),
+                          [&k](uint64_t x, uint64_t y) { return k[x] != k[y] ? k[x] < k[y] : x < y; });
+                SB[a].resize(n);
+                for (uint64_t i = 0; i < n; ++i) SB[a][i] = boxes[S[a][i]];
+            });
+        }
+        for (auto& t : th) t.join();
+        left_flag.assign(n, 0);
+        tmp_i.resize(n);
+        tmp_b.resize(n);
+        bwd_score.resize(n);
     }
-    uint64_t build(uint64_t lo, uint64_t hi, uint32_t level) {  // build_nodes (bvh.rs:75-113)
-        depth = std::max(depth, level);
-        uint64_t n = hi - lo;
-        Box3 box = box_empty();
-        for (uint64_t i = lo; i < hi; ++i) box_extend(box, boxes[idx[i]]);
+    // leaf: order[lo..hi) from axis list `a` (-1: list order = ascending index)
+    uint64_t leaf(Out& o, uint64_t lo, uint64_t hi, int a, const Box3& box) {
         HostNode node;
         node.box = box;
-        if (n <= 4) {
-            node.start = lo; node.end = hi;
-            nodes.push_back(node);
-            return nodes.size() - 1;
+        node.start = lo; node.end = hi;
+        if (a >= 0) {
+            for (uint64_t i = lo; i < hi; ++i) order[i] = S[a][i];
+        } else {
+            for (uint64_t i = lo; i < hi; ++i) order[i] = S[0][i];
+            std::sort(order.begin() + lo, order.begin() + hi);
         }
+        o.nodes.push_back(node);
+        return o.nodes.size() - 1;
+    }
+    // split_ok: in the calling thread's top tree (jobs build their subtree whole)
+    uint64_t build(Out& o, uint64_t lo, uint64_t hi, uint32_t level, int parent_axis, bool split_ok) {
+        const uint64_t n = hi - lo;
+        if (split_ok && par_level && level == par_level && n >= par_min) {  // split off: built later, concurrently
+            jobs.push_back(Job{lo, hi, level, parent_axis, {}});
+            o.nodes.push_back(HostNode{box_empty(), -2 - (int64_t)(jobs.size() - 1), -1, 0, 0});
+            return o.nodes.size() - 1;
+        }
+        o.depth = std::max(o.depth, level);
+        Box3 box = box_empty();  // in the reference's element order (matters only for NaN coordinates)
+        if (parent_axis >= 0) for (uint64_t i = lo; i < hi; ++i) box_extend(box, SB[parent_axis][i]);
+        else for (uint64_t i = lo; i < hi; ++i) box_extend(box, boxes[i]);  // root: list order
+        if (n <= 4) return leaf(o, lo, hi, parent_axis, box);
         uint64_t best_first = n;
         double best = score(box) * (double)n;
         int best_axis = -1;
+        double* bs = bwd_score.data() + lo;
         for (int axis = 0; axis < 3; ++axis) {  // subdivision_score (bvh.rs:120-135)
-            sort_axis(lo, hi, axis);
-            Box3 acc = box_empty();  // AABBSplitsBuilder::make_splits (bvh.rs:238-255)
-            for (uint64_t i = 0; i + 1 < n; ++i) { box_extend(acc, boxes[idx[lo + i]]); fwd[i] = acc; }
+            // AABBSplitsBuilder::make_splits (bvh.rs:238-255): the suffix boxes are only
+            // ever scored, so keep their scores and fold the prefix sweep into the
+            // comparison — the same score() of the same boxes, in the same order.
+            const Box3* sb = SB[axis].data() + lo;
+            Box3 acc = box_empty();
+            for (uint64_t k = 0; k + 1 < n; ++k) { box_extend(acc, sb[n - 1 - k]); bs[k] = score(acc); }
             acc = box_empty();
-            for (uint64_t k = 0; k + 1 < n; ++k) { box_extend(acc, boxes[idx[hi - 1 - k]]); bwd[k] = acc; }
             for (uint64_t i = 0; i + 1 < n; ++i) {
+                box_extend(acc, sb[i]);
                 uint64_t lc = i + 1, rc = n - lc;
-                double s = score(fwd[i]) * (double)lc + score(bwd[(n - 1) - i - 1]) * (double)rc;
-                if (s < best) { best_first = lc; best = s; best_axis = axis; }
+                double sc = score(acc) * (double)lc + bs[(n - 1) - i - 1] * (double)rc;
+                if (sc < best) { best_first = lc; best = sc; best_axis = axis; }
             }
         }
-        if (best_axis < 0) {  // SubdivisionType::SameNode (bvh.rs:93-96)
-            node.start = lo; node.end = hi;
-            nodes.push_back(node);
-            return nodes.size() - 1;
+        if (best_axis < 0) return leaf(o, lo, hi, 2, box);  // SameNode (bvh.rs:93-96): last sort was axis 2
+        // split: the first best_first of the best axis go left; stable-partition the others
+        const uint64_t mid = lo + best_first;
+        for (uint64_t i = lo; i < mid; ++i) left_flag[S[best_axis][i]] = 1;
+        for (int a = 0; a < 3; ++a) {
+            if (a == best_axis) continue;
+            uint64_t* s = S[a].data();
+            Box3* sb = SB[a].data();
+            uint64_t l = lo, r = lo;
+            for (uint64_t i = lo; i < hi; ++i) {
+                const uint64_t p = s[i];
+                if (left_flag[p]) { s[l] = p; sb[l] = sb[i]; ++l; }
+                else { tmp_i[r] = p; tmp_b[r] = sb[i]; ++r; }
+            }
+            std::copy(tmp_i.begin() + lo, tmp_i.begin() + r, s + l);
+            std::copy(tmp_b.begin() + lo, tmp_b.begin() + r, sb + l);
         }
-        sort_axis(lo, hi, best_axis);  // bvh.rs:102
-        uint64_t me = nodes.size();
-        nodes.push_back(node);  // placeholder (bvh.rs:104-105)
-        uint64_t l = build(lo, lo + best_first, level + 1);
-        uint64_t r = build(lo + best_first, hi, level + 1);
-        nodes[me].left = (int64_t)l;
-        nodes[me].right = (int64_t)r;
+        for (uint64_t i = lo; i < mid; ++i) left_flag[S[best_axis][i]] = 0;
+        uint64_t me = o.nodes.size();
+        o.nodes.push_back(HostNode{box, -1, -1, 0, 0});  // placeholder (bvh.rs:104-105)
+        uint64_t l = build(o, lo, mid, level + 1, best_axis, split_ok);
+        uint64_t r = build(o, mid, hi, level + 1, best_axis, split_ok);
+        o.nodes[me].left = (int64_t)l;
+        o.nodes[me].right = (int64_t)r;
+        return me;
+    }
+    // top tree + finished jobs -> one array in the reference's pre-order
+    int64_t emit(const Out& top, uint64_t i, std::vector<HostNode>& dst, uint32_t& depth) {
+        const HostNode& n = top.nodes[i];
+        if (n.left <= -2) {  // a job's subtree: copy, shifting its links
+            const Out& jo = jobs[(size_t)(-2 - n.left)].out;
+            const int64_t off = (int64_t)dst.size();
+            for (HostNode c : jo.nodes) {
+                if (c.left >= 0) { c.left += off; c.right += off; }
+                dst.push_back(c);
+            }
+            depth = std::max(depth, jo.depth);
+            return off;
+        }
+        const int64_t me = (int64_t)dst.size();
+        dst.push_back(n);
+        if (n.left >= 0) {
+            const int64_t l = emit(top, (uint64_t)n.left, dst, depth);
+            const int64_t r = emit(top, (uint64_t)n.right, dst, depth);
+            dst[me].left = l;
+            dst[me].right = r;
+        }
         return me;
     }
 };
@@ -201,17 +299,40 @@ HostBvh build_bvh(const std::vector<Box3>& boxes) {
     h.order.resize(n);
     for (uint64_t i = 0; i < n; ++i) h.order[i] = i;
     if (n == 0) return h;  // BVH over nothing is never traversed (bvh.rs:29,39)
-    Builder b{boxes, {}, h.order, h.nodes, {}, {}, 0};
+    Builder b{boxes, {}, {}, {}, h.order, {}, {}, {}, {}, {}, 0, 0};
     for (int axis = 0; axis < 3; ++axis) {
         b.key[axis].resize(n);
         for (uint64_t i = 0; i < n; ++i)
             b.key[axis][i] = total_key((comp(boxes[i].min, axis) + comp(boxes[i].max, axis)) / 2.0);
     }
-    b.fwd.resize(n > 1 ? n - 1 : 1);
-    b.bwd.resize(n > 1 ? n - 1 : 1);
+    b.presort();
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    if (n >= kParallelBuildMin && hw > 1) {  // subtrees below level 6 built concurrently
+        b.par_level = 6;
+        b.par_min = 4096;
+    }
+    Builder::Out top;
+    top.nodes.reserve(b.par_level ? 256 : 2 * (n / 2 + 1));
+    b.build(top, 0, n, 1, -1, true);
+    if (b.jobs.empty()) {
+        h.nodes = std::move(top.nodes);
+        h.depth = top.depth;
+        return h;
+    }
+    std::atomic<size_t> next{0};
+    std::vector<std::thread> th;
+    const unsigned nt = (unsigned)std::min<size_t>(std::min(hw, 16u), b.jobs.size());
+    for (unsigned t = 0; t < nt; ++t)
+        th.emplace_back([&b, &next] {
+            for (size_t k; (k = next.fetch_add(1)) < b.jobs.size();) {
+                Builder::Job& jb = b.jobs[k];
+                b.build(jb.out, jb.lo, jb.hi, jb.level, jb.parent_axis, false);
+            }
+        });
+    for (auto& t : th) t.join();
     h.nodes.reserve(2 * (n / 2 + 1));
-    b.build(0, n, 1);
-    h.depth = b.depth;
+    h.depth = top.depth;
+    b.emit(top, 0, h.nodes, h.depth);
     return h;
 }
 

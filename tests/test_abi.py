@@ -121,6 +121,26 @@ def test_bvh_builder_matches_oracle(rt, orc, n, grid):
     assert sorted(a[2].tolist()) == list(range(n))
 
 
+@pytest.mark.parametrize("case", ["random", "grid_ties", "identical", "clustered"])
+def test_bvh_parallel_builder_matches_oracle(rt, orc, case):
+    """Above 200k primitives the presorted builder splits subtrees off to threads; the
+    tree must still equal the reference restatement's node for node (incl. leaf order)."""
+    n = 210000
+    rng = np.random.default_rng(11)
+    if case == "random":
+        boxes = _boxes(rng, n)
+    elif case == "grid_ties":      # integer centres: heavy equal-midpoint ties on every axis
+        boxes = _boxes(rng, n, grid=True)
+    elif case == "identical":      # SAH finds no gain at the root: one 210k leaf in axis-2 order
+        boxes = np.tile([0, 0, 0, 1, 1, 1.0], (n, 1))
+    else:                          # a dense cluster plus far outliers (deep, unbalanced tree)
+        boxes = _boxes(rng, n)
+        boxes[: n // 2] *= 1e-3
+    a, b = rt.build_bvh(boxes), orc.build_bvh(boxes)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
+    assert a[3] == b[3]
+
+
 def test_bvh_same_boxes_is_one_leaf(rt):
     """SAH finds no gain on identical boxes -> one leaf holding all of them (bvh.rs:93-96)."""
     boxes = np.tile([0, 0, 0, 1, 1, 1.0], (9, 1))
