@@ -120,6 +120,16 @@ def test_sponza_like_generator_small(rt, tmp_path):
     assert any(m["emission"].max() > 0 for m in desc.materials)
 
 
+def test_hairball_generator_small(rt, tmp_path):
+    gen = os.path.join(REPO, "scenes", "gen_hairball.py")
+    subprocess.run([sys.executable, gen, str(tmp_path), "--tris", "3000", "--name", "hb"], check=True,
+                   capture_output=True)
+    desc, params, _ = assert_same(rt, str(tmp_path / "hb.gltf"), 32, 24, 1)
+    assert len(desc.tri_material) == 3002
+    assert sum(1 for m in desc.materials if m["emission"].max() > 0) == 1
+    assert desc.tri_vertices.reshape(-1, 3)[:-6].__abs__().max() < 1.0  # inside the unit ball
+
+
 def _del(path):
     def f(g):
         obj = g

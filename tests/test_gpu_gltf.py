@@ -33,6 +33,22 @@ def atrium(rt, orc, tmp_path_factory):
     return desc, params, rt.Scene(desc), orc.OracleScene(desc)
 
 
+@pytest.fixture(scope="module")
+def hairball(rt, orc, tmp_path_factory):
+    """gen_hairball at 30k triangles: thin random triangles, deep BVH, one quad light."""
+    d = tmp_path_factory.mktemp("hairball")
+    subprocess.run([sys.executable, os.path.join(REPO, "scenes", "gen_hairball.py"), str(d), "--tris", "30000",
+                    "--name", "hb"], check=True, capture_output=True)
+    desc, params = rt.load_gltf(str(d / "hb.gltf"), 40, 30, 3)
+    return desc, params, rt.Scene(desc), orc.OracleScene(desc)
+
+
+def test_hairball(hairball):
+    desc, params, g, o = hairball
+    img, _, st = _compare(g, o, params)
+    assert st["tri_tests"] > 0 and st["shaded_hits"] > 0
+
+
 def test_room(room):
     desc, params, g, o = room
     img, _, st = _compare(g, o, params)

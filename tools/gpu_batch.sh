@@ -26,6 +26,7 @@ for s in $STEPS; do
     tests) run pytest_gpu 900 python3 -m pytest tests -m gpu -x -q || exit 1 ;;
     c2)    run bench_c2 600 $B --workload C2 --steps 3 --warmup 1 || exit 1 ;;
     c3)    run bench_c3 600 $B --workload C3 --steps 3 --warmup 1 || exit 1 ;;
+    c5)    run bench_c5 900 $B --workload C5 --steps 2 --warmup 1 || exit 1 ;;
     prof2) run prof_c2 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c2" -o run \
              -- $B --workload C2 --steps 2 --warmup 1 --no-cpu-baseline || exit 1 ;;
     prof3) run prof_c3 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c3" -o run \
