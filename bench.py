@@ -4,9 +4,10 @@ hot path on the C2 workload (BASELINE.json configs[1]: Cornell box,
 1920x1080, 256 spp, depth 16) on N MI355X GPUs.
 
 One step = one full frame: every (pixel, sample) path of the frame
-(generate_image, main.rs:85-114, before tonemapping), tile-partitioned across
-the ranks (16x16 tiles round-robin), then ONE RCCL gather of the
-packed framebuffer tiles to rank 0 and the unpack into the row-major image.
+(generate_image, main.rs:85-114), tile-partitioned across the ranks (16x16
+tiles round-robin), then ONE RCCL gather of the packed
+framebuffer tiles to rank 0 and the fused device epilogue: unpack + ACES +
+gamma + PPM bytes (main.rs:104, ppm.rs:13-19) into the row-major payload.
 "Sample" = one path segment = one closest-hit query (raytrace.rs:14); the
 per-frame segment count is counted on the device in an untimed pass.
 
@@ -186,7 +187,8 @@ def main():
     sptr = stream.cuda_stream
     tiles = torch.empty((per, 256, 3), dtype=torch.float64, device=dev)
     gathered = torch.empty((world, per, 256, 3), dtype=torch.float64, device=dev) if rank == 0 else None
-    image = torch.empty((H, W, 3), dtype=torch.float64, device=dev) if rank == 0 else None
+    # the epilogue writes the PPM payload (tonemap + gamma + bytes fused into the unpack)
+    image = torch.empty((H, W, 3), dtype=torch.uint8, device=dev) if rank == 0 else None
 
     # untimed counting pass: this rank's work of one frame
     scene.read_stats(reset=True)
@@ -209,7 +211,7 @@ def main():
             ev.append((e0, e1))
         src = rt.gather_tiles(tiles, gathered, rank, world)
         if rank == 0:
-            rt.unpack_tiles_async(params, world, src.data_ptr(), image.data_ptr(), sptr)
+            rt.unpack_tiles_bytes_async(params, world, src.data_ptr(), image.data_ptr(), sptr)
 
     for _ in range(args.warmup):
         step(False)
@@ -252,6 +254,7 @@ def main():
                 "width": W, "height": H, "spp": spp, "ray_depth": params.ray_depth,
                 "paths_per_step": frame_paths, "segments_per_step": frame_segments,
                 "parallelism": f"tiles16x16 round-robin over {world} GPU(s) + 1 RCCL gather",
+                "epilogue": "device unpack + ACES + gamma + PPM bytes (rt_unpack_tiles_bytes_async)",
                 "seed": params.seed,
             },
             "roofline": {

@@ -115,6 +115,9 @@ EXPORTS = {
     "rt_read_raw_stats": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
     "rt_unpack_tiles_async": (C.c_int, [C.POINTER(rt_render_params), C.c_uint32, C.c_void_p, C.c_void_p,
                                         C.c_void_p]),
+    "rt_unpack_tiles_bytes_async": (C.c_int, [C.POINTER(rt_render_params), C.c_uint32, C.c_void_p, C.c_void_p,
+                                              C.c_void_p]),
+    "rt_tonemap_bytes_async": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),
     "rt_intersect_rays": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]),
     "rt_light_pdf_rays": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]),
     "rt_intersect_lights_rays": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]),
@@ -438,6 +441,19 @@ def gather_tiles(tiles, gathered, rank: int, world: int, group=None):
 def unpack_tiles_async(params: RenderParams, world: int, d_gathered_ptr: int, d_image_ptr: int, stream_ptr: int = 0):
     _check(lib().rt_unpack_tiles_async(C.byref(params.to_c()), world, C.c_void_p(d_gathered_ptr),
                                        C.c_void_p(d_image_ptr), C.c_void_p(stream_ptr)))
+
+
+def unpack_tiles_bytes_async(params: RenderParams, world: int, d_gathered_ptr: int, d_bytes_ptr: int,
+                             stream_ptr: int = 0):
+    """Gathered tiles -> PPM payload [H][W][3] u8 on the device (unpack + tonemap + gamma + bytes)."""
+    _check(lib().rt_unpack_tiles_bytes_async(C.byref(params.to_c()), world, C.c_void_p(d_gathered_ptr),
+                                             C.c_void_p(d_bytes_ptr), C.c_void_p(stream_ptr)))
+
+
+def tonemap_bytes_async(d_rgb_ptr: int, n_pixels: int, d_bytes_ptr: int, stream_ptr: int = 0):
+    """Device correct_gamma(aces_tonemap(.)) + PPM bytes of an HBM-resident mean image."""
+    _check(lib().rt_tonemap_bytes_async(C.c_void_p(d_rgb_ptr), n_pixels, C.c_void_p(d_bytes_ptr),
+                                        C.c_void_p(stream_ptr)))
 
 
 # ------------------------------------------------------- output surface ----

@@ -380,6 +380,23 @@ int rt_unpack_tiles_async(const rt_render_params* p, uint32_t world, const doubl
     return RT_OK;
 }
 
+int rt_unpack_tiles_bytes_async(const rt_render_params* p, uint32_t world, const double* d_gathered,
+                                uint8_t* d_bytes, void* stream) {
+    int rc = check_params(p);
+    if (rc) return rc;
+    if (!d_gathered || !d_bytes || world == 0) return set_error(RT_ERR_INVALID, "bad unpack arguments");
+    KParams k = make_kparams(p, 0, world);
+    HIP_TRY(launch_unpack_bytes(d_gathered, d_bytes, p->width, p->height, k.tiles_x, world, slots_per_rank(k),
+                                (hipStream_t)stream));
+    return RT_OK;
+}
+
+int rt_tonemap_bytes_async(const double* d_rgb, uint64_t n_pixels, uint8_t* d_bytes, void* stream) {
+    if ((!d_rgb || !d_bytes) && n_pixels) return set_error(RT_ERR_INVALID, "rgb/bytes is NULL");
+    HIP_TRY(launch_tonemap_bytes(d_rgb, 3 * n_pixels, d_bytes, (hipStream_t)stream));
+    return RT_OK;
+}
+
 int rt_render(rt_scene* s, const rt_render_params* p, double* out_mean_rgb, int32_t* opt_hit_ids,
               rt_stats* opt_stats) {
     auto t0 = std::chrono::steady_clock::now();

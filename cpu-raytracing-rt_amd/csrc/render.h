@@ -71,6 +71,10 @@ hipError_t launch_intersect(const DevScene& S, const double* rays, uint32_t n, r
                             double* spill_t, hipStream_t st);
 hipError_t launch_light(const DevScene& S, const double* rays, uint32_t n, int mode, double* out, uint32_t* cnt,
                         uint32_t* spill_n, double* spill_t, hipStream_t st);
+// post_dev.hip: tonemap + gamma + PPM bytes (standalone, and fused into the unpack)
+hipError_t launch_tonemap_bytes(const double* rgb, uint64_t n_values, uint8_t* out, hipStream_t st);
+hipError_t launch_unpack_bytes(const double* g, uint8_t* bytes, uint32_t W, uint32_t H, uint32_t tiles_x,
+                               uint32_t world, uint32_t per_rank, hipStream_t st);
 hipError_t launch_unpack(const double* g, double* img, uint32_t W, uint32_t H, uint32_t tiles_x, uint32_t world,
                          uint32_t per_rank, hipStream_t st);
 hipError_t launch_fp64_probe(const double* a, const double* b, double* out, uint32_t n, int op, hipStream_t st);

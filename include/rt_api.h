@@ -216,6 +216,16 @@ int rt_read_stats(rt_scene* scene, rt_stats* out, int reset);
    (rank-major, as ncclGather lays it out) -> d_image [H][W][3]. */
 int rt_unpack_tiles_async(const rt_render_params* params, uint32_t world,
                           const double* d_gathered, double* d_image, void* hip_stream);
+/* The same unpack fused with correct_gamma(aces_tonemap(.)) and the PPM byte
+   quantisation (main.rs:104, postprocessing.rs:5-37, ppm.rs:13-19): d_bytes is
+   the P6 payload [H][W][3] u8, so the f64 image never leaves the device.  Uses
+   the device `pow`, which may round differently from the host libm in the last
+   ulp (a byte can move only on a .5 boundary; see tests/test_gpu_post.py). */
+int rt_unpack_tiles_bytes_async(const rt_render_params* params, uint32_t world,
+                                const double* d_gathered, uint8_t* d_bytes, void* hip_stream);
+/* Device tonemap + gamma + PPM bytes of a mean-radiance image already in HBM
+   ([n_pixels][3] f64 -> [n_pixels][3] u8). */
+int rt_tonemap_bytes_async(const double* d_rgb, uint64_t n_pixels, uint8_t* d_bytes, void* hip_stream);
 
 /* ======================= ray queries ====================================== */
 /* Closest hit for a batch of world rays [n][6] = (origin, dir) — replaces
