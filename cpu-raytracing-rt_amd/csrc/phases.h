@@ -15,7 +15,7 @@ namespace rt {
 // the ratio of the two is the region's lane utilisation.
 enum { kPhAssign, kPhIntersect, kPhLightSample, kPhLightPdf, kPhSegment, kPhCommit, kPhTile,
        kPhTravWave, kPhTravLane, kPhLeafWave, kPhLeafLane, kPhRngWave, kPhRngLane, kPhW0,
-       kPhN = kPhW0 + 5 };
+       kPhPlanes = kPhW0 + 5, kPhBoxes, kPhElls, kPhTris, kPhMaterialise, kPhN };
 constexpr int kPhW = kPhW0 - kPhIntersect;  // weighted word of region k = k + kPhW (k in 1..5)
 #ifdef RT_PHASES
 __shared__ unsigned long long g_phase[kPhN];

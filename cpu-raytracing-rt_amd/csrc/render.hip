@@ -239,35 +239,45 @@ RT_D bool scene_intersect(const DevScene& S, V3 o, V3 d, Stack& stk, Cnt<ST>& C,
     best.valid = false; best.t = 0.0; best.u = best.v = 0.0; best.prim = 0; best.aux = 0; best.kind = 0;
     const Rcp3 rc = make_rcp3(d);
     const bool rfast = ray_fast(o, rc);
+    unsigned long long ph = PH_T();
     for (uint32_t i = 0; i < S.n_planes; ++i) {  // :45-49
         double t; uint32_t aux;
         C.shape();
         if (!shape_closest<0>(S.planes[i], o, d, rc, t, aux)) continue;
         if (!best.valid || t < best.t) { best.valid = true; best.t = t; best.prim = i; best.aux = aux; best.kind = 0; }
     }
+    PH_ADD(kPhPlanes, ph);
+    ph = PH_T();
     {
         double t, u, v; uint32_t p, aux = 0;
         if (bvh_closest_sel<1, ST>(S.boxes, rfast, o, d, rc, stk, C, t, u, v, p, aux) && (!best.valid || t < best.t)) {
             best.valid = true; best.t = t; best.prim = p; best.aux = aux; best.kind = 1;
         }
     }
+    PH_ADD(kPhBoxes, ph);
+    ph = PH_T();
     {
         double t, u, v; uint32_t p, aux = 0;
         if (bvh_closest_sel<2, ST>(S.ells, rfast, o, d, rc, stk, C, t, u, v, p, aux) && (!best.valid || t < best.t)) {
             best.valid = true; best.t = t; best.prim = p; best.aux = aux; best.kind = 2;
         }
     }
+    PH_ADD(kPhElls, ph);
+    ph = PH_T();
     {
         double t, u = 0.0, v = 0.0; uint32_t p, aux = 0;
         if (bvh_closest_sel<3, ST>(S.tris, rfast, o, d, rc, stk, C, t, u, v, p, aux) && (!best.valid || t < best.t)) {
             best.valid = true; best.t = t; best.prim = p; best.u = u; best.v = v; best.aux = 0; best.kind = 3;
         }
     }
+    PH_ADD(kPhTris, ph);
     if (!best.valid) return false;
     if (!(best.t * magnitude(d) <= INFINITY)) return false;  // :56
+    ph = PH_T();
     Quat rot;
     Hit h = materialise(S, best, o, d, rot, mat, gid);
     out = rotated(h, rot);
+    PH_ADD(kPhMaterialise, ph);
     C.shaded();
     return true;
 }

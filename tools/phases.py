@@ -19,7 +19,8 @@ from conftest import load_package  # noqa: E402
 NAMES = ["assign", "intersect", "light_sample", "light_pdf", "segment", "commit", "tile",
          "trav_wave_iters", "trav_lane_iters", "leaf_wave_trips", "leaf_lane_tests",
          "rng_wave_refills", "rng_lane_refills",
-         "w_intersect", "w_light_sample", "w_light_pdf", "w_segment", "w_commit"]
+         "w_intersect", "w_light_sample", "w_light_pdf", "w_segment", "w_commit",
+         "isect_planes", "isect_boxes", "isect_ellipsoids", "isect_triangles", "isect_materialise"]
 rt = load_package()
 wl = sys.argv[1]
 scene_file, W, H, spp, depth = bench.WORKLOADS[wl]
@@ -35,6 +36,8 @@ shading = ph["segment"] - ph["intersect"] - ph["light_sample"] - ph["light_pdf"]
 share = {k: ph[k] / tile for k in ("assign", "intersect", "light_sample", "light_pdf", "commit")}
 share["shading_rest"] = shading / tile
 share["loop_other"] = 1.0 - ph["assign"] / tile - ph["segment"] / tile - ph["commit"] / tile
+for k in ("isect_planes", "isect_boxes", "isect_ellipsoids", "isect_triangles", "isect_materialise"):
+    share[k] = ph[k] / tile
 print(json.dumps({"workload": wl, "spp": spp, "segments": st["segments"],
                   "lane_util": st["lane_steps"] / max(1, st["wave_steps"]),
                   "traversal_loop_util": ph["trav_lane_iters"] / max(1, 64 * ph["trav_wave_iters"]),
