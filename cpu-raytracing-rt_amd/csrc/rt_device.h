@@ -225,8 +225,34 @@ RT_D double safe_max(double a, double b) {
 }
 // FAST: the ray passed ray_fast() and the BVH's boxes DevBvh::fast — every
 // slab quotient takes the unguarded exact division (no d == 0 axis either).
+//
+// In FAST mode the test reduces, exactly, to six quotients and plain min/max:
+//   * no d == 0 axis and every quotient finite (operands in range), so the
+//     safe_min/safe_max guards never fire;
+//   * no NaN, so rmin/rmax equal v_min/v_max up to the sign of a zero result,
+//     which no comparison observes;
+//   * the inside test folds into max(t_near, 0): inside => t_near <= 0 <= t_far
+//     (every axis has min - o <= 0 <= max - o); not inside => some axis has both
+//     quotients of one sign, nonzero (|min - o| >= 2^-449), so either
+//     t_near > 0 or t_far < 0 (a miss);
+//   * so hit <=> t_near <= t_far && 0 <= t_far, and t = max(t_near, 0).
+// (The host sets DevBvh::fast only when every box has min <= max per axis.)
+RT_D bool aabb_hit_fast(V3 mn, V3 mx, V3 o, const Rcp3& rc, V3 d, double& t) {
+    const double ax = fdiv_fast(mn.x - o.x, d.x, rc.r.x), bx = fdiv_fast(mx.x - o.x, d.x, rc.r.x);
+    const double ay = fdiv_fast(mn.y - o.y, d.y, rc.r.y), by = fdiv_fast(mx.y - o.y, d.y, rc.r.y);
+    const double az = fdiv_fast(mn.z - o.z, d.z, rc.r.z), bz = fdiv_fast(mx.z - o.z, d.z, rc.r.z);
+    const double tn = __builtin_fmax(__builtin_fmax(__builtin_fmin(ax, bx), __builtin_fmin(ay, by)),
+                                     __builtin_fmin(az, bz));
+    const double tf = __builtin_fmin(__builtin_fmin(__builtin_fmax(ax, bx), __builtin_fmax(ay, by)),
+                                     __builtin_fmax(az, bz));
+    t = __builtin_fmax(tn, 0.0);
+    return tn <= tf && 0.0 <= tf;
+}
 template <bool FAST = false>
 RT_D bool aabb_hit(V3 mn, V3 mx, V3 o, V3 d, const Rcp3& rc, double& t) {
+#ifndef RT_SLOW_AABB  // ablation build: the literal form for FAST too
+    if (FAST) return aabb_hit_fast(mn, mx, o, rc, d, t);
+#endif
     if (!FAST && ((d.x == 0.0 && (o.x < mn.x || mx.x < o.x)) || (d.y == 0.0 && (o.y < mn.y || mx.y < o.y)) ||
                   (d.z == 0.0 && (o.z < mn.z || mx.z < o.z))))
         return false;

@@ -247,6 +247,8 @@ void flatten(const HostBvh& h, HostBvhArrays& out) {
     for (const HostNode& n : h.nodes) {
         const double c[6] = {n.box.min.x, n.box.min.y, n.box.min.z, n.box.max.x, n.box.max.y, n.box.max.z};
         for (double v : c) fast = fast && coord_fast(v);
+        // aabb_hit_fast's per-axis min/max folding needs min <= max
+        fast = fast && n.box.min.x <= n.box.max.x && n.box.min.y <= n.box.max.y && n.box.min.z <= n.box.max.z;
     }
     out.fast = fast;
 }
