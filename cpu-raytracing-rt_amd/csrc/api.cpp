@@ -269,6 +269,8 @@ int rt_scene_create(const rt_scene_desc* desc, rt_scene** out) {
     HostScene hs;
     std::string err = build_scene(*desc, hs);
     if (!err.empty()) return set_error(RT_ERR_INVALID, err);
+    for (int k = 0; k < 6; ++k)  // traversal stack words carry node indices in 30 bits (render.hip child_word)
+        if (hs.bvh[k].nodes.size() >= (1u << 30)) return set_error(RT_ERR_INVALID, "BVH exceeds 2^30 nodes");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
         return set_error(RT_ERR_DEVICE, "no HIP device visible (the hot path has no CPU fallback)");

@@ -15,7 +15,8 @@ namespace rt {
 // the ratio of the two is the region's lane utilisation.
 enum { kPhAssign, kPhIntersect, kPhLightSample, kPhLightPdf, kPhSegment, kPhCommit, kPhTile,
        kPhTravWave, kPhTravLane, kPhLeafWave, kPhLeafLane, kPhRngWave, kPhRngLane, kPhW0,
-       kPhPlanes = kPhW0 + 5, kPhBoxes, kPhElls, kPhTris, kPhMaterialise, kPhN };
+       kPhPlanes = kPhW0 + 5, kPhBoxes, kPhElls, kPhTris, kPhMaterialise,
+       kPhInnerWave, kPhInnerLane, kPhLiveLane, kPhN };
 constexpr int kPhW = kPhW0 - kPhIntersect;  // weighted word of region k = k + kPhW (k in 1..5)
 #ifdef RT_PHASES
 __shared__ unsigned long long g_phase[kPhN];
@@ -32,6 +33,7 @@ __shared__ unsigned long long g_phase[kPhN];
         if (PH_FIRST()) atomicAdd(&g_phase[kw], 1ull);                                       \
         atomicAdd(&g_phase[kl], 1ull);                                                       \
     } while (0)
+#define PH_LANE(kl) atomicAdd(&g_phase[kl], 1ull)
 #define PH_ADDW(k, t0)                                                                       \
     do {                                                                                     \
         const unsigned long long dt_ = PH_T() - (t0);                                        \
@@ -46,6 +48,7 @@ __shared__ unsigned long long g_phase[kPhN];
 #define PH_ADD(k, t0) ((void)(t0))
 #define PH_ADDW(k, t0) ((void)(t0))
 #define PH_COUNT(kw, kl) ((void)0)
+#define PH_LANE(kl) ((void)0)
 #endif
 
 }  // namespace rt

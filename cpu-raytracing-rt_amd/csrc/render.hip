@@ -51,10 +51,16 @@ struct Stack {
         else { gn[(size_t)(sp - kShort) * stride] = node; gt[(size_t)(sp - kShort) * stride] = t; }
         ++sp;
     }
+    // The spill side reads through volatile pointers: otherwise the compiler
+    // merges the two branches into one select-of-pointers + flat load, which
+    // puts every pop (LDS in > 99% of cases) on the flat path.
     RT_D void pop(uint32_t& node, double& t) {
         --sp;
         if (sp < kShort) { node = sn[sp * kWave]; t = st[sp * kWave]; }
-        else { node = gn[(size_t)(sp - kShort) * stride]; t = gt[(size_t)(sp - kShort) * stride]; }
+        else {
+            node = ((volatile const uint32_t*)gn)[(size_t)(sp - kShort) * stride];
+            t = ((volatile const double*)gt)[(size_t)(sp - kShort) * stride];
+        }
     }
 };
 RT_D Stack make_stack(uint32_t* s_n, double* s_t, uint32_t tid, uint64_t gtid, uint32_t* spill_n, double* spill_t,
@@ -99,6 +105,18 @@ RT_D bool shape_closest(const DevShape& s, V3 o, V3 d, const Rcp3& rc, double& t
     return false;
 }
 
+// Stack word of a pushed child (bvh_closest).  A leaf whose range fits is
+// packed as 1|count(7)|start(24), so resuming it loads nothing; an internal
+// child is its node index (count 0 is known); a leaf that does not fit is its
+// node index | kLeafRef, and its range is loaded on resume.  Node indices are
+// < 2^30 (checked by the host).
+constexpr uint32_t kPackedLeaf = 0x80000000u, kLeafRef = 0x40000000u;
+RT_D uint32_t child_word(uint32_t node, uint32_t start, uint32_t count) {
+    if (count == 0) return node;
+    if (count < 128u && start < (1u << 24)) return kPackedLeaf | (count << 24) | start;
+    return node | kLeafRef;
+}
+
 // BVH::intersection (bvh.rs:27-36) + Node::intersection (bvh.rs:151-186)
 template <int KIND, bool ST, bool FAST>
 RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stack& S, Cnt<ST>& C, double& bt_out,
@@ -125,6 +143,7 @@ RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stack& S, Cnt
         const uint64_t at_leaf = __ballot(live && cnt != 0);
         const bool do_leaves = at_leaf == lv || __popcll(at_leaf) >= kLeafBatch;
         PH_COUNT(kPhTravWave, kPhTravLane);
+        if (live) PH_LANE(kPhLiveLane);
         bool next = false;  // this lane finished its current node and pops
         if (do_leaves) {
             if (live && cnt != 0) {
@@ -142,7 +161,10 @@ RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stack& S, Cnt
                 next = true;
             }
         } else if (live && cnt == 0) {  // internal node (count 0 <=> children)
+            PH_COUNT(kPhInnerWave, kPhInnerLane);
             const DevNode& n = B.nodes[node];
+            // the link words and the children's ranges, with the boxes (one 128-B line)
+            const uint4 links = *(const uint4*)&n.left, kids = *(const uint4*)&n.lstart;
             double lt = 0.0, rt2 = 0.0;
             C.aabb(2);
             bool lh = aabb_hit<FAST>(load3(n.lmin), load3(n.lmax), o, d, rc, lt);
@@ -150,29 +172,32 @@ RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stack& S, Cnt
             const double bt = best;  // +inf when no hit yet
             const double li = lh ? (lt < bt ? lt : bt) : bt;
             const double ri = rh ? (rt2 < bt ? rt2 : bt) : bt;
-            const uint32_t left = (uint32_t)n.left, right = (uint32_t)n.right;
+            const uint32_t left = links.x, right = links.y;
             bool go_left = false;
             if (li < bt) {
                 if (ri < bt) {
-                    if (li < ri) { S.push(right, ri); go_left = true; }
-                    else S.push(left, li);
+                    if (li < ri) { S.push(child_word(right, kids.z, kids.w), ri); go_left = true; }
+                    else S.push(child_word(left, kids.x, kids.y), li);
                 } else go_left = true;
             } else if (!(ri < bt)) next = true;
             if (!next) {
                 node = go_left ? left : right;
-                cnt = go_left ? n.lcount : n.rcount;
-                start = go_left ? n.lstart : n.rstart;
+                cnt = go_left ? kids.y : kids.w;
+                start = go_left ? kids.x : kids.z;
             }
         }
         if (next) {  // resume from the stack: far children still closer than best
             bool found = false;
+            uint32_t w = 0;
             while (S.sp > 0) {
-                uint32_t nn; double tt;
-                S.pop(nn, tt);
-                if (tt < best) { node = nn; found = true; break; }
+                double tt;
+                S.pop(w, tt);
+                if (tt < best) { found = true; break; }
             }
-            if (found) { cnt = B.nodes[node].count; start = B.nodes[node].start; }
-            else live = false;
+            if (!found) live = false;
+            else if (w & kPackedLeaf) { cnt = (w >> 24) & 127u; start = w & 0xFFFFFFu; }
+            else if (w & kLeafRef) { node = w & ~kLeafRef; cnt = B.nodes[node].count; start = B.nodes[node].start; }
+            else { node = w; cnt = 0; }
         }
     }
     if (valid) bt_out = best;

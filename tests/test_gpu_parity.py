@@ -220,3 +220,55 @@ def test_empty_scene_is_background(rt, orc):
     assert np.all(img == np.array([0.25, 0.5, 1.0]))
     assert np.all(hits[:, :, 0] == rt.RT_HIT_MISS) and np.all(hits[:, :, 1:] == rt.RT_HIT_NONE)
     _compare(g, orc.OracleScene(desc), params)
+
+
+def _deep_chain(rt, n=200, cluster=149, g=1.3):
+    """Coplanar triangles (y = 0) at geometrically growing z steps plus a cluster
+    of identical ones: the reference builder makes a 21-level tree with a
+    149-triangle leaf.  Rays lying in the plane hit every box and no triangle
+    (det == 0), so the traversal stack grows to the tree depth — past the LDS
+    short stack (spill) — and the big leaf takes the unpacked stack word
+    (render.hip child_word).  A wall at the far end gives the rays a hit."""
+    tris, z = [], 0.0
+    for i in range(n):
+        w = 0.01 * g ** i
+        tris.append([(-1, 0, z), (1, 0, z), (0, 0, z + 0.5 * w)])
+        if i == n // 2:
+            tris += [[(-0.5, 0, z + 0.1 * w), (0.5, 0, z + 0.1 * w), (0, 0, z + 0.2 * w)]] * cluster
+        z += w
+    tris.append([(-3, -3, 1.5 * z), (3, -3, 1.5 * z), (0, 3, 1.5 * z)])
+    v = np.array(tris, float)
+    m = len(v)
+    nrm = np.tile([0.0, 1.0, 0.0], (m, 3, 1))
+    mats = np.zeros(2, rt.MATERIAL_DTYPE)
+    mats[0]["color"] = [0.6, 0.6, 0.6]
+    mats[1]["emission"] = [1.0, 1.0, 1.0]
+    return rt.SceneDesc(materials=mats, shapes=np.zeros(0, rt.SHAPE_DTYPE), tri_vertices=v.reshape(m, 9),
+                        tri_normals=nrm.reshape(m, 9), tri_material=(np.arange(m) % 2).astype(np.uint32),
+                        tri_mode=rt.RT_TRI_GLTF)
+
+
+def test_deep_stack_and_big_leaf(rt, orc):
+    desc = _deep_chain(rt)
+    g, o = rt.Scene(desc), orc.OracleScene(desc)
+    info = g.info()
+    assert info["bvh_depth"][2] > 12 + 6, info["bvh_depth"]   # the stack spills past the LDS part
+    links, _, _, _ = rt.build_bvh(_tri_boxes(desc))
+    assert (links[:, 3] - links[:, 2]).max() >= 128             # a leaf that does not pack
+    rng = np.random.default_rng(12)
+    n = 4096
+    orig = np.stack([rng.uniform(-0.9, 0.9, n), np.zeros(n), np.full(n, -1.0)], axis=1)
+    d = np.stack([rng.uniform(-1e-6, 1e-6, n), np.zeros(n), np.ones(n)], axis=1)
+    d[: n // 2, 0] = 0.0
+    rays = np.concatenate([orig, d], axis=1)
+    gh, oh = g.intersect(rays), o.intersect(rays)
+    assert np.array_equal(gh.view(np.uint8), oh.view(np.uint8))
+    assert (gh["prim"][: n // 2] == len(desc.tri_material) - 1).all()   # straight rays reach the far wall
+    pd = rays.copy()
+    pd[:, 3:] /= np.linalg.norm(pd[:, 3:], axis=1, keepdims=True)
+    assert np.array_equal(g.light_pdf(pd), o.light_pdf(pd))
+
+
+def _tri_boxes(desc):
+    v = desc.tri_vertices.reshape(-1, 3, 3)
+    return np.concatenate([v.min(1), v.max(1)], axis=1)
