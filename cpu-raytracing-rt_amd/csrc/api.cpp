@@ -210,6 +210,18 @@ uint32_t path_waves(const rt_scene* s) {
     return nodes > kDeepSceneNodes ? 4u : 3u;
 }
 
+// Resumable triangle traversal (path_kernel RES) for scenes with a
+// deep triangle BVH, where a wave's traversal loop otherwise runs most trips
+// with few live lanes (C3: 43%); scenes without one keep the fused segment,
+// which carries less state across the loop (C2: 113 vs 130 ms at 64 spp).
+// RT_RESUME=0|1 forces one (tests, tuning).
+bool path_resume(const rt_scene* s) {
+    if (const char* e = std::getenv("RT_RESUME")) {
+        if (e[0] == '0' || e[0] == '1') return e[0] == '1';
+    }
+    return s->info.bvh_nodes[2] > kDeepSceneNodes;
+}
+
 // Workspace of one path-kernel launch: persistent grid size, then the spill,
 // ring and chunk-partial buffers sized for it (all grow-only, scene-owned).
 int prepare_path(rt_scene* s, const KParams& k, bool stats, bool hits, PathWork& W) {
@@ -217,7 +229,8 @@ int prepare_path(rt_scene* s, const KParams& k, bool stats, bool hits, PathWork&
     if (n_units >= (1ull << 31)) return set_error(RT_ERR_INVALID, "frame too large for one launch");
     std::memset(&W, 0, sizeof(W));
     W.waves = path_waves(s);
-    HIP_TRY(path_grid(stats, hits, W.waves, (uint32_t)n_units, &W.grid));
+    W.resume = path_resume(s);
+    HIP_TRY(path_grid(stats, hits, W.waves, W.resume, (uint32_t)n_units, &W.grid));
     int rc;
     if ((rc = ensure_spill(s, (uint64_t)W.grid * 64)) || (rc = ensure_part(s, k))) return rc;
     if (!s->queue) HIP_TRY(hipMalloc(&s->queue, kQueueWords * sizeof(uint32_t)));

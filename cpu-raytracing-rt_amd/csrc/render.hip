@@ -33,6 +33,10 @@ constexpr int kShort = kMaxBvhDepthShort;
 #define RT_LEAF_BATCH 16  // lanes waiting at leaves before the wave tests primitives (bvh_closest)
 #endif
 constexpr int kLeafBatch = RT_LEAF_BATCH;
+#ifndef RT_SUSPEND
+#define RT_SUSPEND 16  // live lanes below which the path kernel suspends triangle traversal
+#endif
+constexpr int kSuspend = RT_SUSPEND;
 
 // ---------------------------------------------------------------- stack ---
 // LDS short stack laid out per wave: [wave][slot][lane], so consecutive lanes
@@ -117,7 +121,132 @@ RT_D uint32_t child_word(uint32_t node, uint32_t start, uint32_t count) {
     return node | kLeafRef;
 }
 
-// BVH::intersection (bvh.rs:27-36) + Node::intersection (bvh.rs:151-186)
+// BVH::intersection (bvh.rs:27-36) + Node::intersection (bvh.rs:151-186) as
+// a resumable per-lane state: the path kernel suspends a lane's triangle
+// traversal when few lanes of its wave are still traversing,
+// lets the finished lanes shade and start their next segments, and resumes.
+// Each lane's own sequence of visits, tests, `best` updates and pruning is the
+// reference's (bvh.rs:151-210) whatever the suspension points.
+struct Trav {
+    double best, bu, bv;           // closest candidate so far (best = +inf when none)
+    uint32_t prim, aux;
+    uint32_t node, cnt, start;     // current node; its primitive range (cnt 0 = internal)
+    bool valid, live;
+};
+
+// slab test of one box: SLAB 0 = guarded form, 1 = unguarded exact division
+// (DevBvh::fast boxes and a ray_fast ray), 2 = per lane (`fast`)
+template <int SLAB>
+RT_D bool slab(const double* mn, const double* mx, V3 o, V3 d, const Rcp3& rc, bool fast, double& t) {
+    if (SLAB == 1 || (SLAB == 2 && fast)) return aabb_hit<true>(load3(mn), load3(mx), o, d, rc, t);
+    return aabb_hit<false>(load3(mn), load3(mx), o, d, rc, t);
+}
+
+template <int SLAB, bool ST>
+RT_D void trav_init(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stack& S, Cnt<ST>& C, Trav& T) {
+    T.valid = false; T.live = false;
+    T.best = INFINITY; T.bu = T.bv = 0.0; T.prim = 0; T.aux = 0;
+    T.node = 0; T.cnt = 0; T.start = 0;
+    S.sp = 0;
+    if (B.n_prims == 0) return;
+    double t0;
+    C.aabb();
+    if (!slab<SLAB>(B.root_min, B.root_max, o, d, rc, fast, t0)) return;
+    T.cnt = B.nodes[0].count; T.start = B.nodes[0].start;
+    T.live = true;
+}
+
+// One wave-level step for the live lanes (lv = their ballot).  Deferred
+// leaves: a lane that reaches a leaf waits there while the other lanes keep
+// stepping through internal nodes; the wave tests leaf primitives once
+// >= kLeafBatch lanes wait (or every live lane does), so the primitive loop
+// runs with many lanes instead of a few.
+template <int KIND, int SLAB, bool ST>
+RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stack& S, Cnt<ST>& C, Trav& T,
+                    uint64_t lv) {
+    const uint64_t at_leaf = __ballot(T.live && T.cnt != 0);
+    const bool do_leaves = at_leaf == lv || __popcll(at_leaf) >= kLeafBatch;
+    PH_COUNT(kPhTravWave, kPhTravLane);
+    if (T.live) PH_LANE(kPhLiveLane);
+    bool next = false;  // this lane finished its current node and pops
+    if (do_leaves) {
+        if (T.live && T.cnt != 0) {
+            for (uint32_t i = T.start; i < T.start + T.cnt; ++i) {
+                PH_COUNT(kPhLeafWave, kPhLeafLane);
+                double t, u = 0.0, v = 0.0;
+                uint32_t aux = 0;
+                bool h;
+                if (KIND == 3) { C.tri(); h = tri_uvt(B.tris[i], o, d, u, v, t); }
+                else { C.shape(); h = shape_closest<KIND>(B.shapes[i], o, d, rc, t, aux); }
+                if (h && (!T.valid || t < T.best)) {  // update_best_intersection (bvh.rs:213-222)
+                    T.valid = true; T.best = t; T.bu = u; T.bv = v; T.prim = i; T.aux = aux;
+                }
+            }
+            next = true;
+        }
+    } else if (T.live && T.cnt == 0) {  // internal node (count 0 <=> children)
+        PH_COUNT(kPhInnerWave, kPhInnerLane);
+        const DevNode& n = B.nodes[T.node];
+        // the link words and the children's ranges, with the boxes (one 128-B line)
+        const uint4 links = *(const uint4*)&n.left, kids = *(const uint4*)&n.lstart;
+        double lt = 0.0, rt2 = 0.0;
+        C.aabb(2);
+        const bool lh = slab<SLAB>(n.lmin, n.lmax, o, d, rc, fast, lt);
+        const bool rh = slab<SLAB>(n.rmin, n.rmax, o, d, rc, fast, rt2);
+        const double bt = T.best;  // +inf when no hit yet
+        const double li = lh ? (lt < bt ? lt : bt) : bt;
+        const double ri = rh ? (rt2 < bt ? rt2 : bt) : bt;
+        const uint32_t left = links.x, right = links.y;
+        bool go_left = false;
+        if (li < bt) {
+            if (ri < bt) {
+                if (li < ri) { S.push(child_word(right, kids.z, kids.w), ri); go_left = true; }
+                else S.push(child_word(left, kids.x, kids.y), li);
+            } else go_left = true;
+        } else if (!(ri < bt)) next = true;
+        if (!next) {
+            T.node = go_left ? left : right;
+            T.cnt = go_left ? kids.y : kids.w;
+            T.start = go_left ? kids.x : kids.z;
+        }
+    }
+    if (next) {  // resume from the stack: far children still closer than best
+        bool found = false;
+        uint32_t w = 0;
+        while (S.sp > 0) {
+            double tt;
+            S.pop(w, tt);
+            if (tt < T.best) { found = true; break; }
+        }
+        if (!found) T.live = false;
+        else if (w & kPackedLeaf) { T.cnt = (w >> 24) & 127u; T.start = w & 0xFFFFFFu; }
+        else if (w & kLeafRef) {
+            T.node = w & ~kLeafRef; T.cnt = B.nodes[T.node].count; T.start = B.nodes[T.node].start;
+        } else { T.node = w; T.cnt = 0; }
+    }
+}
+
+// BVH::intersection (bvh.rs:27-36) + Node::intersection (bvh.rs:151-186) run
+// to completion, in two code forms with the same steps: TF = false is one
+// self-contained loop (the fused kernel: C2 113 ms at 64 spp vs 116 through
+// Trav), TF = true runs trav_init/trav_step (the resumable kernel, whose
+// register allocation it suits better: C3 364 vs 375 ms).  Only the compiler's
+// view differs; every lane's visits, tests and updates are identical.
+template <int KIND, bool ST, bool FAST>
+RT_D bool bvh_closest_tf(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stack& S, Cnt<ST>& C, double& bt_out,
+                         double& bu, double& bv, uint32_t& bprim, uint32_t& baux) {
+    constexpr int SL = FAST ? 1 : 0;
+    Trav T;
+    trav_init<SL, ST>(B, o, d, rc, FAST, S, C, T);
+    for (;;) {
+        const uint64_t lv = __ballot(T.live);
+        if (lv == 0) break;
+        trav_step<KIND, SL, ST>(B, o, d, rc, FAST, S, C, T, lv);
+    }
+    if (T.valid) { bt_out = T.best; bu = T.bu; bv = T.bv; bprim = T.prim; baux = T.aux; }
+    return T.valid;
+}
+
 template <int KIND, bool ST, bool FAST>
 RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stack& S, Cnt<ST>& C, double& bt_out,
                       double& bu, double& bv, uint32_t& bprim, uint32_t& baux) {
@@ -206,9 +335,13 @@ RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stack& S, Cnt
 
 // Slab tests with the unguarded exact division when the BVH's boxes and this
 // ray allow it (DevBvh::fast, ray_fast); the guarded form otherwise.
-template <int KIND, bool ST>
+template <int KIND, bool ST, bool TF = false>
 RT_D bool bvh_closest_sel(const DevBvh& B, bool rfast, V3 o, V3 d, const Rcp3& rc, Stack& S, Cnt<ST>& C,
                           double& bt_out, double& bu, double& bv, uint32_t& bprim, uint32_t& baux) {
+    if constexpr (TF) {
+        if (B.fast && rfast) return bvh_closest_tf<KIND, ST, true>(B, o, d, rc, S, C, bt_out, bu, bv, bprim, baux);
+        return bvh_closest_tf<KIND, ST, false>(B, o, d, rc, S, C, bt_out, bu, bv, bprim, baux);
+    }
     if (B.fast && rfast) return bvh_closest<KIND, ST, true>(B, o, d, rc, S, C, bt_out, bu, bv, bprim, baux);
     return bvh_closest<KIND, ST, false>(B, o, d, rc, S, C, bt_out, bu, bv, bprim, baux);
 }
@@ -256,14 +389,14 @@ RT_D Hit materialise(const DevScene& S, const Cand& c, V3 o, V3 d, Quat& rot, ui
     return h;
 }
 
-// intersect(ray, &scene.primitives, +inf) (intersections.rs:42-62)
-template <bool ST>
-RT_D bool scene_intersect(const DevScene& S, V3 o, V3 d, Stack& stk, Cnt<ST>& C, Hit& out, uint32_t& mat,
-                          int32_t& gid) {
-    Cand best;
+// intersect(ray, &scene.primitives, +inf) (intersections.rs:42-62) in three
+// parts, so the path kernel can traverse the triangle BVH resumably:
+// shapes_closest (planes, boxes, ellipsoids: :45-55), take_tri (triangles
+// last, strict <: :55), intersect_tail (:56-61).
+template <bool ST, bool TF>
+RT_D void shapes_closest(const DevScene& S, V3 o, V3 d, const Rcp3& rc, bool rfast, Stack& stk, Cnt<ST>& C,
+                         Cand& best) {
     best.valid = false; best.t = 0.0; best.u = best.v = 0.0; best.prim = 0; best.aux = 0; best.kind = 0;
-    const Rcp3 rc = make_rcp3(d);
-    const bool rfast = ray_fast(o, rc);
     unsigned long long ph = PH_T();
     for (uint32_t i = 0; i < S.n_planes; ++i) {  // :45-49
         double t; uint32_t aux;
@@ -275,7 +408,7 @@ RT_D bool scene_intersect(const DevScene& S, V3 o, V3 d, Stack& stk, Cnt<ST>& C,
     ph = PH_T();
     {
         double t, u, v; uint32_t p, aux = 0;
-        if (bvh_closest_sel<1, ST>(S.boxes, rfast, o, d, rc, stk, C, t, u, v, p, aux) && (!best.valid || t < best.t)) {
+        if (bvh_closest_sel<1, ST, TF>(S.boxes, rfast, o, d, rc, stk, C, t, u, v, p, aux) && (!best.valid || t < best.t)) {
             best.valid = true; best.t = t; best.prim = p; best.aux = aux; best.kind = 1;
         }
     }
@@ -283,28 +416,43 @@ RT_D bool scene_intersect(const DevScene& S, V3 o, V3 d, Stack& stk, Cnt<ST>& C,
     ph = PH_T();
     {
         double t, u, v; uint32_t p, aux = 0;
-        if (bvh_closest_sel<2, ST>(S.ells, rfast, o, d, rc, stk, C, t, u, v, p, aux) && (!best.valid || t < best.t)) {
+        if (bvh_closest_sel<2, ST, TF>(S.ells, rfast, o, d, rc, stk, C, t, u, v, p, aux) && (!best.valid || t < best.t)) {
             best.valid = true; best.t = t; best.prim = p; best.aux = aux; best.kind = 2;
         }
     }
     PH_ADD(kPhElls, ph);
-    ph = PH_T();
-    {
-        double t, u = 0.0, v = 0.0; uint32_t p, aux = 0;
-        if (bvh_closest_sel<3, ST>(S.tris, rfast, o, d, rc, stk, C, t, u, v, p, aux) && (!best.valid || t < best.t)) {
-            best.valid = true; best.t = t; best.prim = p; best.u = u; best.v = v; best.aux = 0; best.kind = 3;
-        }
+}
+RT_D void take_tri(Cand& best, bool valid, double t, double u, double v, uint32_t p) {
+    if (valid && (!best.valid || t < best.t)) {
+        best.valid = true; best.t = t; best.prim = p; best.u = u; best.v = v; best.aux = 0; best.kind = 3;
     }
-    PH_ADD(kPhTris, ph);
+}
+template <bool ST>
+RT_D bool intersect_tail(const DevScene& S, const Cand& best, V3 o, V3 d, Cnt<ST>& C, Hit& out, uint32_t& mat,
+                         int32_t& gid) {
     if (!best.valid) return false;
     if (!(best.t * magnitude(d) <= INFINITY)) return false;  // :56
-    ph = PH_T();
+    const unsigned long long ph = PH_T();
     Quat rot;
     Hit h = materialise(S, best, o, d, rot, mat, gid);
     out = rotated(h, rot);
     PH_ADD(kPhMaterialise, ph);
     C.shaded();
     return true;
+}
+template <bool ST>
+RT_D bool scene_intersect(const DevScene& S, V3 o, V3 d, Stack& stk, Cnt<ST>& C, Hit& out, uint32_t& mat,
+                          int32_t& gid) {
+    const Rcp3 rc = make_rcp3(d);
+    const bool rfast = ray_fast(o, rc);
+    Cand best;
+    shapes_closest<ST, false>(S, o, d, rc, rfast, stk, C, best);
+    const unsigned long long ph = PH_T();
+    double t, u = 0.0, v = 0.0; uint32_t p = 0, aux = 0;
+    const bool th = bvh_closest_sel<3, ST>(S.tris, rfast, o, d, rc, stk, C, t, u, v, p, aux);
+    take_tri(best, th, t, u, v, p);
+    PH_ADD(kPhTris, ph);
+    return intersect_tail<ST>(S, best, o, d, C, out, mat, gid);
 }
 
 // ---------------------------------------------------------- light pdf ----
@@ -477,16 +625,35 @@ struct PathState {
     V3 L;          // radiance of this path so far
 };
 
-// One segment of raytrace_impl (raytrace.rs:12-60) in throughput form.
-// Returns true when the path continues with the updated ray.
+// The closest-hit query of one segment, held across path-loop trips while the
+// lane's triangle traversal is suspended (path_kernel): the ray's reciprocals,
+// the best plane/box/ellipsoid candidate and the triangle-BVH traversal state.
+struct SegQuery {
+    Rcp3 rc;
+    Cand best;
+    Trav T;
+    bool fast;  // unguarded slab division for the triangle BVH (DevBvh::fast && ray_fast)
+};
+
+// raytrace_impl's `intersect` call (raytrace.rs:13), first part: planes,
+// boxes and ellipsoids to completion, then the triangle traversal is set up.
 template <bool ST>
-RT_D bool segment(const DevScene& S, const KParams& P, const Scales& sc, PathState& ps, Rng& rng,
-                  Stack& stk, Cnt<ST>& C, int32_t& hit_gid) {
-    Hit h; uint32_t mat; int32_t gid;
+RT_D void segment_begin(const DevScene& S, const PathState& ps, Stack& stk, Cnt<ST>& C, SegQuery& q) {
     C.segment();
-    const unsigned long long ph0 = PH_T();
-    const bool hit = scene_intersect<ST>(S, ps.o, ps.d, stk, C, h, mat, gid);
-    PH_ADDW(kPhIntersect, ph0);
+    q.rc = make_rcp3(ps.d);
+    const bool rfast = ray_fast(ps.o, q.rc);
+    shapes_closest<ST, true>(S, ps.o, ps.d, q.rc, rfast, stk, C, q.best);
+    q.fast = S.tris.fast && rfast;
+    trav_init<2, ST>(S.tris, ps.o, ps.d, q.rc, q.fast, stk, C, q.T);
+}
+
+// One segment of raytrace_impl (raytrace.rs:12-60) in throughput form, from
+// the closest-hit result on.  Returns true when the path continues with the
+// updated ray.
+template <bool ST>
+RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, PathState& ps, Rng& rng,
+                        Stack& stk, Cnt<ST>& C, bool hit, const Hit& h, uint32_t mat, int32_t gid,
+                        int32_t& hit_gid) {
     if (!hit) {
         hit_gid = RT_HIT_MISS;
         ps.L = ps.L + mul(ps.T, load3(P.bg));
@@ -562,6 +729,28 @@ RT_D bool segment(const DevScene& S, const KParams& P, const Scales& sc, PathSta
     return true;
 }
 
+// the resumable form's end of a segment: finish `intersect`, then shade
+template <bool ST>
+RT_D bool segment_end(const DevScene& S, const KParams& P, const Scales& sc, PathState& ps, Rng& rng,
+                      Stack& stk, Cnt<ST>& C, SegQuery& q, int32_t& hit_gid) {
+    Hit h; uint32_t mat = 0; int32_t gid = 0;
+    take_tri(q.best, q.T.valid, q.T.best, q.T.bu, q.T.bv, q.T.prim);
+    const bool hit = intersect_tail<ST>(S, q.best, ps.o, ps.d, C, h, mat, gid);
+    return segment_shade<ST>(S, P, sc, ps, rng, stk, C, hit, h, mat, gid, hit_gid);
+}
+
+// the fused form: one whole segment (scene_intersect to completion, then shade)
+template <bool ST>
+RT_D bool segment(const DevScene& S, const KParams& P, const Scales& sc, PathState& ps, Rng& rng, Stack& stk,
+                  Cnt<ST>& C, int32_t& hit_gid) {
+    Hit h; uint32_t mat; int32_t gid;
+    C.segment();
+    const unsigned long long ph0 = PH_T();
+    const bool hit = scene_intersect<ST>(S, ps.o, ps.d, stk, C, h, mat, gid);
+    PH_ADDW(kPhIntersect, ph0);
+    return segment_shade<ST>(S, P, sc, ps, rng, stk, C, hit, h, mat, gid, hit_gid);
+}
+
 template <bool ST>
 RT_D void wave_flush(const Cnt<ST>& C, unsigned long long* stats, uint32_t wave_iters) {
     if (!ST) return;
@@ -609,7 +798,7 @@ RT_D const T* opaque(const T* p) {
     return p;
 }
 
-template <bool ST, bool HIT, int WAVES>
+template <bool ST, bool HIT, int WAVES, bool RES>
 __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams Pv,
                                                      const DevScene* __restrict__ Sg,
                                                      const KParams* __restrict__ Pg, double* __restrict__ out,
@@ -657,6 +846,9 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
         uint64_t pixel = 0;
         PathState ps;
         Rng rng;
+        SegQuery q;
+        q.T.live = false;
+        bool inq = false;  // this lane's segment query is under way
         for (;;) {
             // 3 waves: fields scalar-loaded where used (see opaque).  4 waves: the
             // by-value kernel arguments, which measured faster at its 128-VGPR
@@ -699,8 +891,46 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
                 next = min(limit, next + (uint32_t)__popcll(idle));
             }
             PH_ADD(kPhAssign, ph_a);
-            // one segment of every live path
-            if (busy) {
+            bool ends = false;  // this lane's path ends in this trip
+            if constexpr (RES) {
+                // lanes between segments (new paths, continued paths) start their query
+                const unsigned long long ph_b = PH_T();
+                if (busy && !inq && b < depth) {
+                    segment_begin<ST>(S, ps, stk, C, q);
+                    inq = true;
+                }
+                PH_ADDW(kPhIntersect, ph_b);
+                // Triangle traversal, resumable: step while enough lanes are live; once
+                // fewer than kSuspend are, and other lanes wait to shade or to take a new
+                // path, suspend the live ones (their stacks and Trav stay put) so the
+                // waiting lanes run now and rejoin the traversal with their next rays.
+                const unsigned long long ph_t = PH_T();
+                for (;;) {
+                    const uint64_t lv = __ballot(q.T.live);
+                    if (lv == 0) break;
+                    if (__popcll(lv) < kSuspend) {
+                        const bool can_take = next < min(total, (base + kRing) * kWave);
+                        if (__ballot((busy && !q.T.live) || (!busy && can_take))) break;
+                    }
+                    trav_step<3, 2, ST>(S.tris, ps.o, ps.d, q.rc, q.fast, stk, C, q.T, lv);
+                }
+                PH_ADD(kPhTris, ph_t);
+                // lanes whose query finished shade and end (or continue) their segment
+                if (busy && !q.T.live) {
+                    C.step();
+                    bool cont = false;
+                    if (inq) {
+                        int32_t g;
+                        const unsigned long long ph_s = PH_T();
+                        cont = segment_end<ST>(S, P, sc, ps, rng, stk, C, q, g);
+                        PH_ADDW(kPhSegment, ph_s);
+                        if (HIT) hit_ids[(pixel * P.spp + s) * depth + b] = g;
+                        ++b;
+                        inq = false;
+                    }
+                    ends = !cont || b >= depth;
+                }
+            } else if (busy) {  // fused: one whole segment of every live path
                 C.step();
                 bool cont = false;
                 if (b < depth) {
@@ -719,6 +949,14 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
                     atomicAdd(&s_cnt[r], 1u);
                     busy = false;
                 }
+            }
+            if (RES && ends) {
+                if (HIT) for (uint32_t k = b; k < depth; ++k) hit_ids[(pixel * P.spp + s) * depth + k] = RT_HIT_NONE;
+                const uint32_t r = (cur / kWave) % kRing;
+                double* rp = ring + ((uint64_t)r * kWave + cur % kWave) * 3;
+                rp[0] = ps.L.x; rp[1] = ps.L.y; rp[2] = ps.L.z;
+                atomicAdd(&s_cnt[r], 1u);
+                busy = false;
             }
             ++witers;
             // commit complete rows in sample order (ring stores visible to the wave)
@@ -815,21 +1053,23 @@ __global__ void fp64_probe_kernel(const double* a, const double* b, double* out,
 namespace {
 using PathFn = void (*)(DevScene, KParams, const DevScene*, const KParams*, double*, double*, int32_t*,
                         unsigned long long*, uint32_t*, double*, uint32_t*, double*);
-PathFn path_fn(bool stats, bool hits, uint32_t waves) {
-    static const PathFn tab[8] = {path_kernel<false, false, 3>, path_kernel<false, false, 4>,
-                                  path_kernel<false, true, 3>,  path_kernel<false, true, 4>,
-                                  path_kernel<true, false, 3>,  path_kernel<true, false, 4>,
-                                  path_kernel<true, true, 3>,   path_kernel<true, true, 4>};
-    return tab[(stats ? 4 : 0) + (hits ? 2 : 0) + (waves == 4 ? 1 : 0)];
+template <bool ST, bool HIT>
+PathFn path_fn_r(uint32_t waves, bool resume) {
+    if (waves == 4) return resume ? path_kernel<ST, HIT, 4, true> : path_kernel<ST, HIT, 4, false>;
+    return resume ? path_kernel<ST, HIT, 3, true> : path_kernel<ST, HIT, 3, false>;
+}
+PathFn path_fn(bool stats, bool hits, uint32_t waves, bool resume) {
+    if (stats) return hits ? path_fn_r<true, true>(waves, resume) : path_fn_r<true, false>(waves, resume);
+    return hits ? path_fn_r<false, true>(waves, resume) : path_fn_r<false, false>(waves, resume);
 }
 }  // namespace
 
-hipError_t path_grid(bool stats, bool hits, uint32_t waves, uint32_t n_units, uint32_t* grid) {
+hipError_t path_grid(bool stats, bool hits, uint32_t waves, bool resume, uint32_t n_units, uint32_t* grid) {
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e != hipSuccess) return e;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)path_fn(stats, hits, waves), kWave, 0);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)path_fn(stats, hits, waves, resume), kWave, 0);
     if (e != hipSuccess) return e;
     const uint64_t g = (uint64_t)std::max(per_cu, 1) * (uint64_t)std::max(cus, 1);
     *grid = (uint32_t)std::min<uint64_t>(g, std::max<uint32_t>(n_units, 1u));
@@ -849,7 +1089,7 @@ hipError_t launch_path(const DevScene& S, const KParams& P, const PathWork& W, d
     hipLaunchKernelGGL(stage_params_kernel, dim3(1), dim3(1), 0, st, W.d_params, P);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(path_fn(stats != nullptr, hit_ids != nullptr, W.waves), dim3(W.grid), dim3(kWave), 0, st,
+    hipLaunchKernelGGL(path_fn(stats != nullptr, hit_ids != nullptr, W.waves, W.resume), dim3(W.grid), dim3(kWave), 0, st,
                        S, P, W.d_scene, W.d_params, out, W.part, hit_ids, stats, W.spill_n, W.spill_t, W.queue, W.ring);
     e = hipGetLastError();
     if (e != hipSuccess || P.chunks == 1) return e;

@@ -11,7 +11,7 @@ import pytest
 
 from conftest import REPO
 import gltf_scenes
-from test_gpu_parity import _compare
+from test_gpu_parity import _compare, segment_form  # noqa: F401 (autouse: both segment forms)
 
 pytestmark = pytest.mark.gpu
 

@@ -30,6 +30,15 @@ def sink(rt, orc, scene_text):
     return desc, params, rt.Scene(desc), orc.OracleScene(desc)
 
 
+@pytest.fixture(autouse=True, params=["fused", "resume"])
+def segment_form(request, monkeypatch):
+    """Every test runs both path-kernel segment forms: fused (whole closest-hit
+    query, then shading) and resumable (triangle traversal suspended while few
+    lanes are live); the host picks one per scene (RT_RESUME)."""
+    monkeypatch.setenv("RT_RESUME", "1" if request.param == "resume" else "0")
+    return request.param
+
+
 def _compare(gpu_scene, ora_scene, params):
     from conftest import load_package
     _, chunk_spp = load_package().sample_chunks(params)

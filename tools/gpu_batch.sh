@@ -63,7 +63,7 @@ for s in $STEPS; do
     lane3) run lane_C3 600 python3 tools/lane_util.py C3 64 64 32 8 || exit 1 ;;
     var2|var3)  # every cpu-raytracing-rt_amd/build*/librt_amd.so variant at reduced spp
       w=C${s#var}
-      run variants_$w 900 python3 tools/variants.py $w ${VAR_SPP:-64} cpu-raytracing-rt_amd/build*/librt_amd.so \
+      run variants_$w 900 python3 tools/variants.py $w ${VAR_SPP:-64} ${VARIANTS:-cpu-raytracing-rt_amd/build*/librt_amd.so} \
         || exit 1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

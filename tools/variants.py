@@ -1,6 +1,7 @@
 """Time alternate builds of librt_amd.so on a bench workload at reduced spp.
-usage: python tools/variants.py WORKLOAD SPP lib1.so lib2.so ...   (each lib in its own process)
-WORKLOAD is a bench.py workload name (C1, C2, C3, ...)."""
+usage: python tools/variants.py WORKLOAD SPP lib1.so lib2.so[@VAR=val,VAR2=val] ...   (each in its own process)
+WORKLOAD is a bench.py workload name (C1, C2, C3, ...); `@VAR=val,...` sets environment overrides
+(e.g. RT_WAVES=3, RT_RESUME=0) for that run."""
 import os
 import subprocess
 import sys
@@ -24,13 +25,15 @@ ks = []
 for i in range(3):
     _, _, st2 = s.generate_image(params)
     ks.append(st2["kernel_ms"])
-print(json.dumps({"lib": os.environ["RT_AMD_LIB"], "workload": sys.argv[2], "spp": params.spp, "kernel_ms": ks,
+print(json.dumps({"lib": os.environ["RT_AMD_LIB"], "env": os.environ.get("RT_VARIANT_ENV", ""), "workload": sys.argv[2], "spp": params.spp, "kernel_ms": ks,
                   "Mseg_s": st["segments"] / min(ks) / 1e3, "segments": st["segments"]}))
 '''
 wl, spp = sys.argv[1], sys.argv[2]
 rc = 0
-for lib in sys.argv[3:]:
-    env = dict(os.environ, RT_AMD_LIB=os.path.abspath(lib))
+for arg in sys.argv[3:]:
+    lib, _, over = arg.partition("@")
+    env = dict(os.environ, RT_AMD_LIB=os.path.abspath(lib), RT_VARIANT_ENV=over)
+    env.update(kv.split("=", 1) for kv in over.split(",") if kv)
     r = subprocess.run([sys.executable, "-c", CHILD, os.path.dirname(HERE), wl, spp], env=env, capture_output=True,
                        text=True, timeout=600)
     print(r.stdout.strip() or r.stderr[-2000:], flush=True)
