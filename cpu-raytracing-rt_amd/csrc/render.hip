@@ -43,16 +43,31 @@ constexpr int kSuspend = RT_SUSPEND;
 // hit consecutive banks for any block size.
 constexpr int kWave = 64;
 
+// The pointers are this wave's bases (wave-uniform, so they live in SGPRs);
+// each access adds the lane index, recomputed through an opaque mbcnt so the
+// compiler cannot hoist it into a long-lived VGPR (which it then spilled to
+// scratch and reloaded on every push and pop of the 4-wave path kernel).
+RT_D uint32_t stack_lane() {
+    uint32_t m = ~0u;
+    asm volatile("" : "+s"(m));
+    return __builtin_amdgcn_mbcnt_hi(m, __builtin_amdgcn_mbcnt_lo(m, 0u));
+}
+// OPQ = false keeps the lane index in a register (the 3-wave fused kernel,
+// which has room: C2 113.8 vs 115.1 ms with OPQ); OPQ = true recomputes it.
+template <bool OPQ>
 struct Stack {
-    uint32_t* sn;        // LDS node slots, stride kWave
-    double* st;          // LDS entry-t slots, stride kWave
-    uint32_t* gn;        // global spill (stride = spill_stride) or null
+    uint32_t* sn;        // LDS node slots of this wave, [slot][lane]
+    double* st;          // LDS entry-t slots of this wave, [slot][lane]
+    uint32_t* gn;        // global spill of this wave ([slot][stride], lane-indexed) or null
     double* gt;
     uint32_t stride;
+    uint32_t ln;         // lane index (OPQ = false)
     int sp;
+    RT_D uint32_t lane() const { return OPQ ? stack_lane() : ln; }
     RT_D void push(uint32_t node, double t) {
-        if (sp < kShort) { sn[sp * kWave] = node; st[sp * kWave] = t; }
-        else { gn[(size_t)(sp - kShort) * stride] = node; gt[(size_t)(sp - kShort) * stride] = t; }
+        const uint32_t l = lane();
+        if (sp < kShort) { sn[sp * kWave + l] = node; st[sp * kWave + l] = t; }
+        else { gn[(size_t)(sp - kShort) * stride + l] = node; gt[(size_t)(sp - kShort) * stride + l] = t; }
         ++sp;
     }
     // The spill side reads through volatile pointers: otherwise the compiler
@@ -60,20 +75,25 @@ struct Stack {
     // puts every pop (LDS in > 99% of cases) on the flat path.
     RT_D void pop(uint32_t& node, double& t) {
         --sp;
-        if (sp < kShort) { node = sn[sp * kWave]; t = st[sp * kWave]; }
+        const uint32_t l = lane();
+        if (sp < kShort) { node = sn[sp * kWave + l]; t = st[sp * kWave + l]; }
         else {
-            node = ((volatile const uint32_t*)gn)[(size_t)(sp - kShort) * stride];
-            t = ((volatile const double*)gt)[(size_t)(sp - kShort) * stride];
+            node = ((volatile const uint32_t*)gn)[(size_t)(sp - kShort) * stride + l];
+            t = ((volatile const double*)gt)[(size_t)(sp - kShort) * stride + l];
         }
     }
 };
-RT_D Stack make_stack(uint32_t* s_n, double* s_t, uint32_t tid, uint64_t gtid, uint32_t* spill_n, double* spill_t,
-                      uint32_t spill_stride) {
-    Stack k;
-    const uint32_t base = (tid / kWave) * kShort * kWave + tid % kWave;
+// wave_tid = the wave's first thread in the block, wave_gtid = its first
+// thread in the grid (both wave-uniform)
+template <bool OPQ = false>
+RT_D Stack<OPQ> make_stack(uint32_t* s_n, double* s_t, uint32_t wave_tid, uint64_t wave_gtid, uint32_t* spill_n,
+                           double* spill_t, uint32_t spill_stride) {
+    Stack<OPQ> k;
+    k.ln = __lane_id();
+    const uint32_t base = (wave_tid / kWave) * kShort * kWave;
     k.sn = s_n + base; k.st = s_t + base;
-    k.gn = spill_n ? spill_n + gtid : nullptr;
-    k.gt = spill_t ? spill_t + gtid : nullptr;
+    k.gn = spill_n ? spill_n + wave_gtid : nullptr;
+    k.gt = spill_t ? spill_t + wave_gtid : nullptr;
     k.stride = spill_stride;
     k.sp = 0;
     return k;
@@ -142,8 +162,8 @@ RT_D bool slab(const double* mn, const double* mx, V3 o, V3 d, const Rcp3& rc, b
     return aabb_hit<false>(load3(mn), load3(mx), o, d, rc, t);
 }
 
-template <int SLAB, bool ST>
-RT_D void trav_init(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stack& S, Cnt<ST>& C, Trav& T) {
+template <int SLAB, bool ST, class Stk>
+RT_D void trav_init(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk& S, Cnt<ST>& C, Trav& T) {
     T.valid = false; T.live = false;
     T.best = INFINITY; T.bu = T.bv = 0.0; T.prim = 0; T.aux = 0;
     T.node = 0; T.cnt = 0; T.start = 0;
@@ -161,8 +181,8 @@ RT_D void trav_init(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stac
 // stepping through internal nodes; the wave tests leaf primitives once
 // >= kLeafBatch lanes wait (or every live lane does), so the primitive loop
 // runs with many lanes instead of a few.
-template <int KIND, int SLAB, bool ST>
-RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stack& S, Cnt<ST>& C, Trav& T,
+template <int KIND, int SLAB, bool ST, class Stk>
+RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk& S, Cnt<ST>& C, Trav& T,
                     uint64_t lv) {
     const uint64_t at_leaf = __ballot(T.live && T.cnt != 0);
     const bool do_leaves = at_leaf == lv || __popcll(at_leaf) >= kLeafBatch;
@@ -232,8 +252,8 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stac
 // Trav), TF = true runs trav_init/trav_step (the resumable kernel, whose
 // register allocation it suits better: C3 364 vs 375 ms).  Only the compiler's
 // view differs; every lane's visits, tests and updates are identical.
-template <int KIND, bool ST, bool FAST>
-RT_D bool bvh_closest_tf(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stack& S, Cnt<ST>& C, double& bt_out,
+template <int KIND, bool ST, bool FAST, class Stk>
+RT_D bool bvh_closest_tf(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stk& S, Cnt<ST>& C, double& bt_out,
                          double& bu, double& bv, uint32_t& bprim, uint32_t& baux) {
     constexpr int SL = FAST ? 1 : 0;
     Trav T;
@@ -247,8 +267,8 @@ RT_D bool bvh_closest_tf(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stack& S, 
     return T.valid;
 }
 
-template <int KIND, bool ST, bool FAST>
-RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stack& S, Cnt<ST>& C, double& bt_out,
+template <int KIND, bool ST, bool FAST, class Stk>
+RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stk& S, Cnt<ST>& C, double& bt_out,
                       double& bu, double& bv, uint32_t& bprim, uint32_t& baux) {
     if (B.n_prims == 0) return false;
     double t0;
@@ -335,8 +355,8 @@ RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stack& S, Cnt
 
 // Slab tests with the unguarded exact division when the BVH's boxes and this
 // ray allow it (DevBvh::fast, ray_fast); the guarded form otherwise.
-template <int KIND, bool ST, bool TF = false>
-RT_D bool bvh_closest_sel(const DevBvh& B, bool rfast, V3 o, V3 d, const Rcp3& rc, Stack& S, Cnt<ST>& C,
+template <int KIND, bool ST, bool TF = false, class Stk>
+RT_D bool bvh_closest_sel(const DevBvh& B, bool rfast, V3 o, V3 d, const Rcp3& rc, Stk& S, Cnt<ST>& C,
                           double& bt_out, double& bu, double& bv, uint32_t& bprim, uint32_t& baux) {
     if constexpr (TF) {
         if (B.fast && rfast) return bvh_closest_tf<KIND, ST, true>(B, o, d, rc, S, C, bt_out, bu, bv, bprim, baux);
@@ -393,8 +413,8 @@ RT_D Hit materialise(const DevScene& S, const Cand& c, V3 o, V3 d, Quat& rot, ui
 // parts, so the path kernel can traverse the triangle BVH resumably:
 // shapes_closest (planes, boxes, ellipsoids: :45-55), take_tri (triangles
 // last, strict <: :55), intersect_tail (:56-61).
-template <bool ST, bool TF>
-RT_D void shapes_closest(const DevScene& S, V3 o, V3 d, const Rcp3& rc, bool rfast, Stack& stk, Cnt<ST>& C,
+template <bool ST, bool TF, class Stk>
+RT_D void shapes_closest(const DevScene& S, V3 o, V3 d, const Rcp3& rc, bool rfast, Stk& stk, Cnt<ST>& C,
                          Cand& best) {
     best.valid = false; best.t = 0.0; best.u = best.v = 0.0; best.prim = 0; best.aux = 0; best.kind = 0;
     unsigned long long ph = PH_T();
@@ -440,8 +460,8 @@ RT_D bool intersect_tail(const DevScene& S, const Cand& best, V3 o, V3 d, Cnt<ST
     C.shaded();
     return true;
 }
-template <bool ST>
-RT_D bool scene_intersect(const DevScene& S, V3 o, V3 d, Stack& stk, Cnt<ST>& C, Hit& out, uint32_t& mat,
+template <bool ST, class Stk>
+RT_D bool scene_intersect(const DevScene& S, V3 o, V3 d, Stk& stk, Cnt<ST>& C, Hit& out, uint32_t& mat,
                           int32_t& gid) {
     const Rcp3 rc = make_rcp3(d);
     const bool rfast = ray_fast(o, rc);
@@ -464,8 +484,8 @@ RT_D double prob_ell(V3 r, V3 ng) {
 }
 
 // Node::intersections (bvh.rs:188-210) accumulating the Light::pdf callback
-template <int KIND, bool ST>
-RT_D void bvh_all(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stack& S, Cnt<ST>& C, double& impact,
+template <int KIND, bool ST, class Stk>
+RT_D void bvh_all(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stk& S, Cnt<ST>& C, double& impact,
                   uint32_t& nhits) {
     if (B.n_prims == 0) return;
     double t0;
@@ -544,8 +564,8 @@ RT_D void bvh_all(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stack& S, Cnt<ST>
 }
 
 // intersect_lights (intersections.rs:87-91): boxes, ellipsoids, triangles
-template <bool ST>
-RT_D double lights_impact(const DevScene& S, V3 o, V3 d, Stack& stk, Cnt<ST>& C, uint32_t& nhits) {
+template <bool ST, class Stk>
+RT_D double lights_impact(const DevScene& S, V3 o, V3 d, Stk& stk, Cnt<ST>& C, uint32_t& nhits) {
     double impact = 0.0;
     const Rcp3 rc = make_rcp3(d);  // dead (DCE'd) unless RT_FASTDIV
     bvh_all<1, ST>(S.lboxes, o, d, rc, stk, C, impact, nhits);
@@ -553,8 +573,8 @@ RT_D double lights_impact(const DevScene& S, V3 o, V3 d, Stack& stk, Cnt<ST>& C,
     bvh_all<3, ST>(S.ltris, o, d, rc, stk, C, impact, nhits);
     return impact;
 }
-template <bool ST>
-RT_D double light_pdf(const DevScene& S, V3 pos, V3 dir, Stack& stk, Cnt<ST>& C) {  // ray_sampler.rs:132-139
+template <bool ST, class Stk>
+RT_D double light_pdf(const DevScene& S, V3 pos, V3 dir, Stk& stk, Cnt<ST>& C) {  // ray_sampler.rs:132-139
     C.lq();
     uint32_t nh = 0;
     double impact = lights_impact<ST>(S, pos + dir * kEpsilon, dir, stk, C, nh);
@@ -637,8 +657,8 @@ struct SegQuery {
 
 // raytrace_impl's `intersect` call (raytrace.rs:13), first part: planes,
 // boxes and ellipsoids to completion, then the triangle traversal is set up.
-template <bool ST>
-RT_D void segment_begin(const DevScene& S, const PathState& ps, Stack& stk, Cnt<ST>& C, SegQuery& q) {
+template <bool ST, class Stk>
+RT_D void segment_begin(const DevScene& S, const PathState& ps, Stk& stk, Cnt<ST>& C, SegQuery& q) {
     C.segment();
     q.rc = make_rcp3(ps.d);
     const bool rfast = ray_fast(ps.o, q.rc);
@@ -650,9 +670,9 @@ RT_D void segment_begin(const DevScene& S, const PathState& ps, Stack& stk, Cnt<
 // One segment of raytrace_impl (raytrace.rs:12-60) in throughput form, from
 // the closest-hit result on.  Returns true when the path continues with the
 // updated ray.
-template <bool ST>
+template <bool ST, class Stk>
 RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, PathState& ps, Rng& rng,
-                        Stack& stk, Cnt<ST>& C, bool hit, const Hit& h, uint32_t mat, int32_t gid,
+                        Stk& stk, Cnt<ST>& C, bool hit, const Hit& h, uint32_t mat, int32_t gid,
                         int32_t& hit_gid) {
     if (!hit) {
         hit_gid = RT_HIT_MISS;
@@ -730,9 +750,9 @@ RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, P
 }
 
 // the resumable form's end of a segment: finish `intersect`, then shade
-template <bool ST>
+template <bool ST, class Stk>
 RT_D bool segment_end(const DevScene& S, const KParams& P, const Scales& sc, PathState& ps, Rng& rng,
-                      Stack& stk, Cnt<ST>& C, SegQuery& q, int32_t& hit_gid) {
+                      Stk& stk, Cnt<ST>& C, SegQuery& q, int32_t& hit_gid) {
     Hit h; uint32_t mat = 0; int32_t gid = 0;
     take_tri(q.best, q.T.valid, q.T.best, q.T.bu, q.T.bv, q.T.prim);
     const bool hit = intersect_tail<ST>(S, q.best, ps.o, ps.d, C, h, mat, gid);
@@ -740,8 +760,8 @@ RT_D bool segment_end(const DevScene& S, const KParams& P, const Scales& sc, Pat
 }
 
 // the fused form: one whole segment (scene_intersect to completion, then shade)
-template <bool ST>
-RT_D bool segment(const DevScene& S, const KParams& P, const Scales& sc, PathState& ps, Rng& rng, Stack& stk,
+template <bool ST, class Stk>
+RT_D bool segment(const DevScene& S, const KParams& P, const Scales& sc, PathState& ps, Rng& rng, Stk& stk,
                   Cnt<ST>& C, int32_t& hit_gid) {
     Hit h; uint32_t mat; int32_t gid;
     C.segment();
@@ -810,7 +830,7 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
     __shared__ double s_t[kShort * kWave];
     __shared__ uint32_t s_cnt[kRing];  // finished paths per ring row
     const uint32_t lane = threadIdx.x;
-    Stack stk = make_stack(s_n, s_t, lane, (uint64_t)blockIdx.x * kWave + lane, spill_n, spill_t,
+    auto stk = make_stack<RES>(s_n, s_t, 0u, (uint64_t)blockIdx.x * kWave, spill_n, spill_t,
                            gridDim.x * kWave);
     double* ring = ring_all + (uint64_t)blockIdx.x * kRing * kWave * 3;
     const KParams& Pt = WAVES == 3 ? *Pg : Pv;  // per-wave-tile constants
@@ -995,7 +1015,8 @@ __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S, const dou
     __shared__ double s_t[kShort * kBlock];
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
-    Stack stk = make_stack(s_n, s_t, threadIdx.x, i, spill_n, spill_t, gridDim.x * kBlock);
+    const uint32_t wtid = __builtin_amdgcn_readfirstlane(threadIdx.x) & ~(uint32_t)(kWave - 1);
+    auto stk = make_stack(s_n, s_t, wtid, (uint64_t)blockIdx.x * kBlock + wtid, spill_n, spill_t, gridDim.x * kBlock);
     Cnt<false> C;
     Hit h; uint32_t mat; int32_t gid;
     V3 o = load3(rays + 6 * (size_t)i), d = load3(rays + 6 * (size_t)i + 3);
@@ -1018,7 +1039,8 @@ __global__ __launch_bounds__(kBlock) void light_kernel(DevScene S, const double*
     __shared__ double s_t[kShort * kBlock];
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
-    Stack stk = make_stack(s_n, s_t, threadIdx.x, i, spill_n, spill_t, gridDim.x * kBlock);
+    const uint32_t wtid = __builtin_amdgcn_readfirstlane(threadIdx.x) & ~(uint32_t)(kWave - 1);
+    auto stk = make_stack(s_n, s_t, wtid, (uint64_t)blockIdx.x * kBlock + wtid, spill_n, spill_t, gridDim.x * kBlock);
     Cnt<false> C;
     V3 o = load3(rays + 6 * (size_t)i), d = load3(rays + 6 * (size_t)i + 3);
     uint32_t nh = 0;
