@@ -119,6 +119,7 @@ EXPORTS = {
                                               C.c_void_p]),
     "rt_tonemap_bytes_async": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),
     "rt_intersect_rays": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]),
+    "rt_intersect_rays_async": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_int, C.c_void_p]),
     "rt_light_pdf_rays": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]),
     "rt_intersect_lights_rays": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]),
     "rt_parse_custom_scene": (C.c_int, [C.c_char_p, C.POINTER(C.c_void_p)]),
@@ -376,6 +377,12 @@ class Scene:
         _check(lib().rt_intersect_rays(self._h, rays.ctypes.data_as(C.c_void_p), len(rays),
                                        out.ctypes.data_as(C.c_void_p)))
         return out
+
+    def intersect_async(self, d_rays_ptr: int, n: int, d_hits_ptr: int, method: int = 1, stream_ptr: int = 0):
+        """Device-buffer batch intersect (rt_intersect_rays_async): d_rays [n][6] f64 and
+        d_hits [n] rt_hit (64 B) in HBM; method 0 = one thread per ray, 1 = persistent."""
+        _check(lib().rt_intersect_rays_async(self._h, C.c_void_p(d_rays_ptr), n, C.c_void_p(d_hits_ptr), method,
+                                             C.c_void_p(stream_ptr)))
 
     def light_pdf(self, pos_dir: np.ndarray) -> np.ndarray:
         """Light::pdf for [n, 6] (surface position, unit direction)."""

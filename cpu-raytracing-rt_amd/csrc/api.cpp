@@ -478,6 +478,30 @@ int rt_intersect_rays(rt_scene* s, const double* rays, uint32_t n, rt_hit* out) 
     return RT_OK;
 }
 
+int rt_intersect_rays_async(rt_scene* s, const double* d_rays, uint32_t n, rt_hit* d_out, int method,
+                            void* hip_stream) {
+    if (!s || (!d_rays && n) || (!d_out && n)) return set_error(RT_ERR_INVALID, "bad arguments");
+    if (method != RT_TRACE_PER_RAY && method != RT_TRACE_PERSISTENT) return set_error(RT_ERR_INVALID, "bad method");
+    if (n == 0) return RT_OK;
+    HIP_TRY(hipSetDevice(s->device));
+    const hipStream_t st = (hipStream_t)hip_stream;
+    if (method == RT_TRACE_PER_RAY) {
+        int rc = ensure_spill(s, ((uint64_t)n + 255) / 256 * 256);
+        if (rc) return rc;
+        HIP_TRY(launch_intersect(s->dev, d_rays, n, d_out, s->spill_n, s->spill_t, st));
+        return RT_OK;
+    }
+    uint32_t grid = 0;
+    HIP_TRY(trace_grid(n, &grid));
+    // the ray counter may run past n by one refill per wave: keep it in 32 bits
+    if ((uint64_t)n + (uint64_t)grid * 64 >= (1ull << 32)) return set_error(RT_ERR_INVALID, "too many rays");
+    int rc = ensure_spill(s, (uint64_t)grid * 64);
+    if (rc) return rc;
+    if (!s->queue) HIP_TRY(hipMalloc(&s->queue, kQueueWords * sizeof(uint32_t)));
+    HIP_TRY(launch_trace(s->dev, d_rays, n, d_out, s->queue, s->spill_n, s->spill_t, grid, st));
+    return RT_OK;
+}
+
 static int light_query(rt_scene* s, const double* rays, uint32_t n, int mode, double* out, uint32_t* cnt) {
     if (!s || (!rays && n) || (!out && n)) return set_error(RT_ERR_INVALID, "bad arguments");
     if (n == 0) return RT_OK;

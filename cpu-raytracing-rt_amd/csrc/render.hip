@@ -1008,6 +1008,72 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
 #endif
 }
 
+// trace_kernel — batch `intersect` (intersections.rs:42-62) as a persistent
+// traversal: each wave keeps its lanes busy by fetching the next rays from a
+// global counter as soon as enough lanes have finished (kRefill), so a wave
+// never waits for its slowest ray.  Per ray the steps are those of
+// scene_intersect (shapes to completion, then the resumable triangle traversal
+// in the reference order), so the hits are identical to intersect_kernel's.
+constexpr int kRefill = 16;
+RT_D void write_hit(rt_hit* __restrict__ out, uint32_t i, bool ok, const Hit& h, int32_t gid) {
+    rt_hit r;
+    if (ok) {
+        r.t = h.t; store3(r.geometry_normal, h.ng); store3(r.shading_normal, h.ns);
+        r.inside = h.inside ? 1 : 0; r.prim = gid;
+    } else {
+        r.t = 0.0; store3(r.geometry_normal, v3(0, 0, 0)); store3(r.shading_normal, v3(0, 0, 0));
+        r.inside = 0; r.prim = RT_HIT_MISS;
+    }
+    out[i] = r;
+}
+
+template <int WAVES>
+__global__ __launch_bounds__(kWave, WAVES) void trace_kernel(DevScene S, const double* __restrict__ rays,
+                                                             uint32_t n, rt_hit* __restrict__ out,
+                                                             uint32_t* __restrict__ queue, uint32_t* spill_n,
+                                                             double* spill_t) {
+    __shared__ uint32_t s_n[kShort * kWave];
+    __shared__ double s_t[kShort * kWave];
+    auto stk = make_stack<true>(s_n, s_t, 0u, (uint64_t)blockIdx.x * kWave, spill_n, spill_t, gridDim.x * kWave);
+    Cnt<false> C;
+    const uint64_t below = (1ull << threadIdx.x) - 1ull;
+    bool has = false, drained = false;  // drained: wave-uniform
+    uint32_t idx = 0;
+    PathState ps;
+    SegQuery q;
+    q.T.live = false;
+    for (;;) {
+        const uint64_t idle = __ballot(!has);
+        const uint64_t lv = __ballot(q.T.live);
+        if (!drained && idle && (__popcll(idle) >= kRefill || lv == 0)) {
+            uint32_t b = 0;
+            if (threadIdx.x == 0) b = atomicAdd(queue, (uint32_t)__popcll(idle));
+            const uint32_t base = __builtin_amdgcn_readfirstlane(b);
+            if ((uint64_t)base + (uint64_t)__popcll(idle) >= n) drained = true;
+            if (!has) {
+                const uint32_t k = base + (uint32_t)__popcll(idle & below);
+                if (k < n) {
+                    idx = k;
+                    ps.o = load3(rays + 6 * (size_t)k);
+                    ps.d = load3(rays + 6 * (size_t)k + 3);
+                    segment_begin<false>(S, ps, stk, C, q);
+                    has = true;
+                }
+            }
+        }
+        const uint64_t lv2 = __ballot(q.T.live);
+        if (lv2) trav_step<3, 2, false>(S.tris, ps.o, ps.d, q.rc, q.fast, stk, C, q.T, lv2);
+        if (has && !q.T.live) {
+            Hit h; uint32_t mat = 0; int32_t gid = 0;
+            take_tri(q.best, q.T.valid, q.T.best, q.T.bu, q.T.bv, q.T.prim);
+            const bool ok = intersect_tail<false>(S, q.best, ps.o, ps.d, C, h, mat, gid);
+            write_hit(out, idx, ok, h, gid);
+            has = false;
+        }
+        if (drained && !__ballot(has)) break;
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S, const double* __restrict__ rays, uint32_t n,
                                                            rt_hit* __restrict__ out, uint32_t* spill_n,
                                                            double* spill_t) {
@@ -1142,6 +1208,24 @@ hipError_t launch_intersect(const DevScene& S, const double* rays, uint32_t n, r
     uint32_t blocks = (n + kBlock - 1) / kBlock;
     hipLaunchKernelGGL(intersect_kernel, dim3(blocks), dim3(kBlock), 0, st, S, rays, n, out, spill_n, spill_t);
     return hipGetLastError();
+}
+// persistent batch intersect (trace_kernel): grid = resident waves, capped by the rays
+hipError_t launch_trace(const DevScene& S, const double* rays, uint32_t n, rt_hit* out, uint32_t* queue,
+                        uint32_t* spill_n, double* spill_t, uint32_t grid, hipStream_t st) {
+    hipError_t e = hipMemsetAsync(queue, 0, kQueueWords * sizeof(uint32_t), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(trace_kernel<4>, dim3(grid), dim3(kWave), 0, st, S, rays, n, out, queue, spill_n, spill_t);
+    return hipGetLastError();
+}
+hipError_t trace_grid(uint32_t n, uint32_t* grid) {
+    int dev = 0, cus = 0, per_cu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)trace_kernel<4>, kWave, 0);
+    if (e != hipSuccess) return e;
+    const uint64_t g = (uint64_t)std::max(per_cu, 1) * (uint64_t)std::max(cus, 1);
+    *grid = (uint32_t)std::min<uint64_t>(g, std::max<uint64_t>(((uint64_t)n + kWave - 1) / kWave, 1));
+    return hipSuccess;
 }
 hipError_t launch_light(const DevScene& S, const double* rays, uint32_t n, int mode, double* out, uint32_t* cnt,
                         uint32_t* spill_n, double* spill_t, hipStream_t st) {

@@ -231,6 +231,15 @@ int rt_tonemap_bytes_async(const double* d_rgb, uint64_t n_pixels, uint8_t* d_by
 /* Closest hit for a batch of world rays [n][6] = (origin, dir) — replaces
    intersections.rs:42-62 `intersect(ray, &scene.primitives, +inf)`. */
 int rt_intersect_rays(rt_scene* scene, const double* rays, uint32_t n, rt_hit* out);
+/* The same query on device-resident buffers, stream-ordered (no host copies):
+   d_rays [n][6] f64 and d_out [n] rt_hit in HBM.  method 0 runs one thread per
+   ray; method 1 the persistent traversal (waves refill finished lanes from a
+   queue).  Both give identical hits.  Uses the scene's workspace, so one
+   launch per scene at a time (like rt_render_tiles_async). */
+#define RT_TRACE_PER_RAY    0
+#define RT_TRACE_PERSISTENT 1
+int rt_intersect_rays_async(rt_scene* scene, const double* d_rays, uint32_t n, rt_hit* d_out, int method,
+                            void* hip_stream);
 /* Light-area pdf for a batch [n][6] = (surface pos, unit dir) — replaces
    ray_sampler.rs:132-139 Light::pdf (all-hits query intersections.rs:87-91). */
 int rt_light_pdf_rays(rt_scene* scene, const double* pos_dir, uint32_t n, double* out_pdf);

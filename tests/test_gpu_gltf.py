@@ -11,7 +11,7 @@ import pytest
 
 from conftest import REPO
 import gltf_scenes
-from test_gpu_parity import _compare, segment_form  # noqa: F401 (autouse: both segment forms)
+from test_gpu_parity import _compare, intersect_device, segment_form  # noqa: F401 (autouse: both segment forms)
 
 pytestmark = pytest.mark.gpu
 
@@ -80,6 +80,18 @@ def test_atrium_intersect_random(atrium):
     assert np.array_equal(gh["prim"], oh["prim"])
     assert np.array_equal(gh.view(np.uint8), oh.view(np.uint8))
     assert (gh["prim"] >= 0).mean() > 0.75   # open-roofed atrium: upward rays may escape
+
+
+@pytest.mark.parametrize("method", [0, 1])
+def test_atrium_intersect_device(atrium, rt, method):
+    """Deep triangle BVH through both device batch kernels: the oracle's hits."""
+    desc, params, g, o = atrium
+    rng = np.random.default_rng(14)
+    n = 30000
+    pos = np.stack([rng.uniform(-10, 10, n), rng.uniform(0.5, 11, n), rng.uniform(-5, 5, n)], axis=1)
+    rays = np.concatenate([pos, rng.standard_normal((n, 3))], axis=1)
+    gh, oh = intersect_device(rt, g, rays, method), o.intersect(rays)
+    assert np.array_equal(gh.view(np.uint8), oh.view(np.uint8))
 
 
 def test_atrium_light_pdf_random(atrium):
