@@ -16,7 +16,10 @@
 
 namespace rt {
 
-constexpr int kMaxBvhDepthShort = 12;   // per-lane short stack kept in LDS
+#ifndef RT_SHORT_STACK
+#define RT_SHORT_STACK 12
+#endif
+constexpr int kMaxBvhDepthShort = RT_SHORT_STACK;   // per-lane short stack kept in LDS
 
 struct alignas(128) DevNode {
     double lmin[3], lmax[3];   // left child's box  (bvh.rs:158)
