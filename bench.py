@@ -265,7 +265,7 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "traffic_detail": traffic_detail,
-                "kernel": "rt::path_kernel<false,false,W> (W = waves/SIMD budget chosen for the scene)",
+                "kernel": "rt::path_kernel<false,false,W,RES> (W = waves/SIMD budget, RES = resumable traversal; both chosen per scene)",
                 "kernel_ms": kern_ms,
                 "algorithmic_bytes_per_launch": algo_bytes(st),
                 "bytes_model": "32*aabb_tests + 72*tri_tests + 80*shape_tests + 100*shaded_hits (rank 0 tiles)",
