@@ -276,6 +276,20 @@ RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stk& S, Cnt<S
     if (!aabb_hit<FAST>(load3(B.root_min), load3(B.root_max), o, d, rc, t0)) return false;
     bool valid = false;
     double best = INFINITY;
+    if (B.depth == 1) {  // the root is the only leaf (bvh.rs:77, <= 4 primitives): [0, n_prims) in order
+        for (uint32_t i = 0; i < B.n_prims; ++i) {
+            double t, u = 0.0, v = 0.0;
+            uint32_t aux = 0;
+            bool h;
+            if (KIND == 3) { C.tri(); h = tri_uvt(B.tris[i], o, d, u, v, t); }
+            else { C.shape(); h = shape_closest<KIND>(B.shapes[i], o, d, rc, t, aux); }
+            if (h && (!valid || t < best)) {  // update_best_intersection (bvh.rs:213-222)
+                valid = true; best = t; bu = u; bv = v; bprim = i; baux = aux;
+            }
+        }
+        if (valid) bt_out = best;
+        return valid;
+    }
     uint32_t node = 0;
     S.sp = 0;
     // Deferred leaves: a lane that reaches a leaf waits there while the other
@@ -483,6 +497,61 @@ RT_D double prob_ell(V3 r, V3 ng) {
     return 1.0 / (4.0 * kPi * sqrt(dot(coef, coef)));
 }
 
+// the Light::pdf callback over the primitives [start, start + cnt) of a leaf
+// (bvh.rs:194-198 -> intersection_probability.rs:9-35)
+template <int KIND, bool ST>
+RT_D void leaf_all(const DevBvh& B, uint32_t start, uint32_t cnt, V3 o, V3 d, const Rcp3& rc, Cnt<ST>& C,
+                   double& impact, uint32_t& nhits) {
+    for (uint32_t i = start; i < start + cnt; ++i) {
+        if (KIND == 3) {
+            C.tri();
+            double u, v, t;
+            if (tri_uvt(B.tris[i], o, d, u, v, t)) {
+                V3 ng = load3(B.tri_cold[i].ng);  // sign flip (triangle.rs:76) cancels in |d.n|
+                impact += B.tri_inv_area[i] * (t * t / fabs(dot(d, ng)));
+                C.lhit(); nhits++;
+            }
+        } else {
+            C.shape();
+            const DevShape s = B.shapes[i];
+            V3 mo, md;
+            const bool same = model_ray(s, o, d, mo, md);
+            Quat q = load_quat(s.rot);
+            const bool qid = is_identity(q);
+            V3 sz = load3(s.shape);
+            if (KIND == 1) {
+                Bpi en, ex;
+                int k = box_coef(sz, mo, md, same ? rc : make_rcp3(md), en, ex);
+                const double pb = s.aux[0];
+                if (k == 2) {
+                    V3 ng = normalize(rotate(q, bpi_normal(en)));
+                    impact += pb * (en.t * en.t / fabs(dot(d, ng)));
+                    C.lhit(); nhits++;
+                }
+                if (k >= 1) {
+                    V3 ng = normalize(rotate(q, bpi_normal(ex)));
+                    impact += pb * (ex.t * ex.t / fabs(dot(d, ng)));
+                    C.lhit(); nhits++;
+                }
+            } else {
+                double t1, t2;
+                const Radii R = load_radii(s);
+                int k = ell_coef(R, mo, md, t1, t2);
+                if (k == 2) {
+                    V3 ng = normalize(rotate_fast(q, qid, ell_normal(R, mo, md, t1)));
+                    impact += prob_ell(sz, ng) * (t1 * t1 / fabs(dot(d, ng)));
+                    C.lhit(); nhits++;
+                }
+                if (k >= 1) {
+                    V3 ng = normalize(rotate_fast(q, qid, -ell_normal(R, mo, md, t2)));
+                    impact += prob_ell(sz, ng) * (t2 * t2 / fabs(dot(d, ng)));
+                    C.lhit(); nhits++;
+                }
+            }
+        }
+    }
+}
+
 // Node::intersections (bvh.rs:188-210) accumulating the Light::pdf callback
 template <int KIND, bool ST, class Stk>
 RT_D void bvh_all(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stk& S, Cnt<ST>& C, double& impact,
@@ -491,59 +560,16 @@ RT_D void bvh_all(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stk& S, Cnt<ST>& 
     double t0;
     C.aabb();
     if (!aabb_hit(load3(B.root_min), load3(B.root_max), o, d, rc, t0)) return;
+    if (B.depth == 1) {  // the root is the only leaf: [0, n_prims), no stack
+        leaf_all<KIND, ST>(B, 0u, B.n_prims, o, d, rc, C, impact, nhits);
+        return;
+    }
     uint32_t node = 0;
     S.sp = 0;
     for (;;) {
         const DevNode& n = B.nodes[node];
         const uint32_t cnt = n.count, start = n.start;
-        for (uint32_t i = start; i < start + cnt; ++i) {
-            if (KIND == 3) {
-                C.tri();
-                double u, v, t;
-                if (tri_uvt(B.tris[i], o, d, u, v, t)) {
-                    V3 ng = load3(B.tri_cold[i].ng);  // sign flip (triangle.rs:76) cancels in |d.n|
-                    impact += B.tri_inv_area[i] * (t * t / fabs(dot(d, ng)));
-                    C.lhit(); nhits++;
-                }
-            } else {
-                C.shape();
-                const DevShape s = B.shapes[i];
-                V3 mo, md;
-                const bool same = model_ray(s, o, d, mo, md);
-                Quat q = load_quat(s.rot);
-                const bool qid = is_identity(q);
-                V3 sz = load3(s.shape);
-                if (KIND == 1) {
-                    Bpi en, ex;
-                    int k = box_coef(sz, mo, md, same ? rc : make_rcp3(md), en, ex);
-                    const double pb = s.aux[0];
-                    if (k == 2) {
-                        V3 ng = normalize(rotate(q, bpi_normal(en)));
-                        impact += pb * (en.t * en.t / fabs(dot(d, ng)));
-                        C.lhit(); nhits++;
-                    }
-                    if (k >= 1) {
-                        V3 ng = normalize(rotate(q, bpi_normal(ex)));
-                        impact += pb * (ex.t * ex.t / fabs(dot(d, ng)));
-                        C.lhit(); nhits++;
-                    }
-                } else {
-                    double t1, t2;
-                    const Radii R = load_radii(s);
-                    int k = ell_coef(R, mo, md, t1, t2);
-                    if (k == 2) {
-                        V3 ng = normalize(rotate_fast(q, qid, ell_normal(R, mo, md, t1)));
-                        impact += prob_ell(sz, ng) * (t1 * t1 / fabs(dot(d, ng)));
-                        C.lhit(); nhits++;
-                    }
-                    if (k >= 1) {
-                        V3 ng = normalize(rotate_fast(q, qid, -ell_normal(R, mo, md, t2)));
-                        impact += prob_ell(sz, ng) * (t2 * t2 / fabs(dot(d, ng)));
-                        C.lhit(); nhits++;
-                    }
-                }
-            }
-        }
+        leaf_all<KIND, ST>(B, start, cnt, o, d, rc, C, impact, nhits);
         const int32_t left = n.left;
         if (left >= 0) {
             double lt, rt2;
