@@ -706,6 +706,7 @@ RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, P
         return false;
     }
     hit_gid = gid;
+    rng_align(rng);   // shading draws start on a block boundary (oracle.c rng_align)
     rng_top_up(rng);  // every hit lane here: a coherent refill point
     const DevMaterial& m = S.mats[mat];
     const V3 col = load3(m.color);

@@ -29,7 +29,9 @@ namespace rt {
 // coherent points (rng_top_up: path start, each hit, before the diffuse
 // sampler) and a draw that empties the current block only swaps it in.  The
 // word stream is unchanged — blocks are still produced and consumed in counter
-// order; only when they are computed moves.
+// order; only when they are computed moves.  At each hit the rest of the
+// current block is skipped (rng_align), so the blocks of one shading step line
+// up across lanes.
 struct Rng {
     uint32_t sample, pix_lo, pix_hi, k0, k1;
     uint32_t blk;       // counter of the next block to generate
@@ -74,6 +76,10 @@ RT_D void rng_top_up(Rng& r) {  // coherent refill point (see Rng)
         r.nready = 1;
     }
 }
+// Skip the rest of the current block: the next draw starts a fresh one.  At
+// every hit (oracle.c rng_align), so all lanes start their shading draws on a
+// block boundary and lanes in the same branch refill at the same points.
+RT_D void rng_align(Rng& r) { r.avail = 0; }
 RT_D uint32_t next_u32(Rng& r) {
     if (r.avail == 0) {
         if (!r.nready) philox_next(r);

@@ -736,6 +736,13 @@ static inline uint32_t next_u32(Rng* r) {
     if (r->idx == 4) { oracle_philox4x32_10(r->ctr, r->key, r->buf); r->ctr[0]++; r->idx = 0; }
     return r->buf[r->idx++];
 }
+/* Start the next draw on a fresh 4-word block (the rest of the current one is
+   skipped).  Called at every hit before shading draws anything, so each
+   shading step consumes its words from a block boundary: lanes in the same
+   branch then need new blocks at the same points on the device (coherent
+   Philox refills).  Skipping words of a counter-based stream leaves the draws
+   independent and uniform. */
+static inline void rng_align(Rng* r) { r->idx = 4; }
 static inline uint64_t next_u64(Rng* r) { /* BlockRng::next_u64: lo word then hi word */
     uint64_t lo = next_u32(r);
     uint64_t hi = next_u32(r);
@@ -904,6 +911,7 @@ static V3 raytrace_impl(Ctx* x, V3 o, V3 d, uint32_t left) { /* raytrace.rs:12-6
     int hit = scene_intersect(x->s, o, d, &sh, x->c);
     if (x->hits) x->hits[bounce] = hit ? (int32_t)sh.gid : RT_HIT_MISS;
     if (!hit) return vld(x->p->bg_color);
+    rng_align(x->rng);
     const rt_material* m = &x->s->mats[sh.mat];
     const Hit* h = &sh.h;
     V3 e = vld(m->emission), col = vld(m->color);
@@ -949,6 +957,7 @@ static V3 raytrace_iter(Ctx* x, V3 o, V3 d) {
         int hit = scene_intersect(x->s, o, d, &sh, x->c);
         if (x->hits) x->hits[b] = hit ? (int32_t)sh.gid : RT_HIT_MISS;
         if (!hit) { L = vadd(L, vmul(T, vld(x->p->bg_color))); break; }
+        rng_align(x->rng);
         const rt_material* m = &x->s->mats[sh.mat];
         const Hit* h = &sh.h;
         V3 col = vld(m->color);
