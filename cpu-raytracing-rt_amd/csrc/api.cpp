@@ -302,6 +302,8 @@ int rt_scene_create(const rt_scene_desc* desc, rt_scene** out) {
         return rc;
     }
     d.n_lights = d.lboxes.n_prims + d.lells.n_prims + d.ltris.n_prims;
+    // UINT64_MAX - (2^64 - n) % n (oracle.c usize_zone); unused without lights
+    d.light_zone = d.n_lights ? UINT64_MAX - (0ull - (uint64_t)d.n_lights) % (uint64_t)d.n_lights : 0;
     d.max_depth = 0;
     const DevBvh* all[6] = {&d.boxes, &d.ells, &d.tris, &d.lboxes, &d.lells, &d.ltris};
     for (int k = 0; k < 6; ++k) {

@@ -640,7 +640,7 @@ RT_D V3 uniform_on_box(V3 s, Rng& r, const Scales& sc) {  // ray_sampler.rs:142-
     return mul(p, s);
 }
 RT_D V3 light_sample(const DevScene& S, V3 pos, Rng& r, const Scales& sc) {  // ray_sampler.rs:101-130
-    uint64_t index = gen_index(r, S.n_lights);
+    uint64_t index = gen_index(r, S.n_lights, S.light_zone);
     rng_top_up(r);
     const uint32_t nb = S.lboxes.n_prims, ne = S.lells.n_prims;
     V3 world;

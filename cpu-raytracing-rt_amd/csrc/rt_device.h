@@ -64,6 +64,7 @@ RT_D void rng_init(Rng& r, uint64_t seed, uint64_t pixel, uint32_t sample) {
 // Fallback for the rare draw that finds no next block ready.
 RT_D void philox_next(Rng& r) {
     PH_COUNT(kPhRngWave, kPhRngLane);
+    PH_COUNT(kPhRngFallWave, kPhRngFallLane);
     philox(r.blk, r.sample, r.pix_lo, r.pix_hi, r.k0, r.k1, r.n0, r.n1);
     r.blk++;
     r.nready = 1;
@@ -122,21 +123,18 @@ RT_HD double inclusive_scale(double low, double high) {  // UniformFloat::new_in
     return scale;
 }
 RT_D double gen_range_incl(Rng& r, double low, double scale) { return value0_1(r) * scale + low; }
-RT_D uint64_t gen_index(Rng& r, uint64_t range) {  // UniformInt<usize>::sample_single(0..range)
-    uint64_t zone = (range << __clzll(range)) - 1;
+// UniformInt<usize>::sample_single(0..range) with the exact acceptance zone
+// (host-precomputed: DevScene::light_zone; oracle.c usize_zone)
+RT_D uint64_t gen_index(Rng& r, uint64_t range, uint64_t zone) {
     for (;;) {
         uint64_t v = next_u64(r);
         uint64_t lo = v * range, hi = __umul64hi(v, range);
         if (lo <= zone) return hi;
     }
 }
-RT_D int32_t gen_sign_bit(Rng& r) {  // UniformInt<i32>::sample_single_inclusive(0, 1)
-    for (;;) {
-        uint32_t v = next_u32(r);
-        uint32_t lo = v << 1, hi = v >> 31;
-        if (lo <= 0x7FFFFFFFu) return (int32_t)hi;
-    }
-}
+// UniformInt<i32>::sample_single_inclusive(0, 1) with the exact zone (oracle.c
+// gen_range_i32_0_1): range 2 never rejects, the result is the word's top bit
+RT_D int32_t gen_sign_bit(Rng& r) { return (int32_t)(next_u32(r) >> 31); }
 RT_D bool gen_bool(Rng& r, double p) {  // Bernoulli
     if (p == 1.0) return true;  // ALWAYS_TRUE, no draw
     uint64_t p_int = (p >= 0.0 && p < 1.0) ? (uint64_t)(p * 18446744073709551616.0) : 0ull;

@@ -79,6 +79,7 @@ struct DevBvh {
 struct DevScene {
     uint32_t n_planes;
     uint32_t n_lights;         // boxes + ellipsoids + triangles in the light BVHs
+    uint64_t light_zone;       // exact UniformInt acceptance zone for gen_index(n_lights)
     const DevShape* planes;
     const uint32_t* plane_mat;
     const int32_t* plane_gid;

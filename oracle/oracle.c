@@ -773,10 +773,17 @@ static double gen_range_incl_f64(Rng* r, double low, double high) {
     double scale = incl_scale(low, high);
     return value0_1(r) * scale + low;
 }
+/* UniformInt widening-multiply rejection (rand 0.8.5 uniform.rs sample_single_inclusive)
+   with the EXACT acceptance zone MAX - (MAX - range + 1) % range, the form rand itself
+   uses for u8/u16, instead of its conservative (range << lz) - 1 for wider types.
+   Same uniform output distribution; for power-of-two ranges (1 light, the sign bit)
+   it never rejects, so every lane consumes the same words (coherent device refills),
+   where the conservative zone rejects half the draws. */
+static uint64_t usize_zone(uint64_t range) { return UINT64_MAX - (0 - range) % range; }
 static uint64_t gen_range_usize(Rng* r, uint64_t n) { /* UniformInt<usize>::sample_single(0, n) */
     uint64_t range = n; /* high-1 - low + 1 */
     if (range == 0) return next_u64(r);
-    uint64_t zone = (range << __builtin_clzll(range)) - 1;
+    uint64_t zone = usize_zone(range);
     for (;;) {
         uint64_t v = next_u64(r);
         unsigned __int128 m = (unsigned __int128)v * range;
@@ -786,7 +793,7 @@ static uint64_t gen_range_usize(Rng* r, uint64_t n) { /* UniformInt<usize>::samp
 }
 static int32_t gen_range_i32_0_1(Rng* r) { /* UniformInt<i32>::sample_single_inclusive(0, 1) */
     const uint32_t range = 2;
-    const uint32_t zone = (range << __builtin_clz(range)) - 1;
+    const uint32_t zone = UINT32_MAX - (0u - range) % range; /* exact zone (see usize_zone): no rejection */
     for (;;) {
         uint32_t v = next_u32(r);
         uint64_t m = (uint64_t)v * range;

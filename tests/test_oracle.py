@@ -115,6 +115,12 @@ def test_rand_transforms(orc):
     draws = np.concatenate([orc.sampler_draws(seed, p, 0, 3, [5, 0, 0], 200)[:, 0] for p in range(20)])
     counts = np.bincount(draws.astype(int), minlength=5)
     assert counts.sum() == 4000 and counts.min() > 700
+    # exact acceptance zone: power-of-two ranges never reject, so gen_range(0..2)
+    # is the top bit of each u64 of the stream, one word pair per draw
+    two = orc.sampler_draws(seed, 9, 1, 3, [2, 0, 0], 300)[:, 0]
+    stream = orc.rng_stream_u64(seed, 9, 1, 300)
+    assert np.array_equal(two.astype(np.uint64), stream >> np.uint64(63))
+    assert np.all(orc.sampler_draws(seed, 9, 1, 3, [1, 0, 0], 50)[:, 0] == 0)
     # gen_bool(0.5)
     b = np.concatenate([orc.sampler_draws(seed, p, 1, 4, [0.5, 0, 0], 200)[:, 0] for p in range(20)])
     assert 1800 < b.sum() < 2200
