@@ -523,14 +523,18 @@ RT_D void leaf_all(const DevBvh& B, uint32_t start, uint32_t cnt, V3 o, V3 d, co
                 Bpi en, ex;
                 int k = box_coef(sz, mo, md, same ? rc : make_rcp3(md), en, ex);
                 const double pb = s.aux[0];
+                // |d . normalize(rotate(q, n))| for a face normal n = sign * e_dim.  With an
+                // identity q, rotate returns n up to the signs of its zero components and
+                // normalize leaves a unit axis vector unchanged, so the dot is +-d[dim] up to
+                // signed zeros, which fabs discards: exactly |d[dim]|.
                 if (k == 2) {
-                    V3 ng = normalize(rotate(q, bpi_normal(en)));
-                    impact += pb * (en.t * en.t / fabs(dot(d, ng)));
+                    const double dn = qid ? fabs(comp(d, en.dim)) : fabs(dot(d, normalize(rotate(q, bpi_normal(en)))));
+                    impact += pb * (en.t * en.t / dn);
                     C.lhit(); nhits++;
                 }
                 if (k >= 1) {
-                    V3 ng = normalize(rotate(q, bpi_normal(ex)));
-                    impact += pb * (ex.t * ex.t / fabs(dot(d, ng)));
+                    const double dn = qid ? fabs(comp(d, ex.dim)) : fabs(dot(d, normalize(rotate(q, bpi_normal(ex)))));
+                    impact += pb * (ex.t * ex.t / dn);
                     C.lhit(); nhits++;
                 }
             } else {
