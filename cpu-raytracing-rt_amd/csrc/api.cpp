@@ -301,6 +301,29 @@ int rt_scene_create(const rt_scene_desc* desc, rt_scene** out) {
         free_scene(s);
         return rc;
     }
+    {  // world normals of plane sides and box faces: rotated(Hit, rot) of render.hip materialise
+        std::vector<double> pn(hs.planes.size() * 6), bn(hs.bvh[0].shapes.size() * 24, 0.0);
+        for (size_t i = 0; i < hs.planes.size(); ++i) {
+            const DevShape& p = hs.planes[i];
+            const Quat q = load_quat(p.rot);
+            for (int side = 0; side < 2; ++side)
+                store3(&pn[i * 6 + side * 3], normalize(rotate(q, load3(p.shape) * (side ? 1.0 : -1.0))));
+        }
+        for (size_t i = 0; i < hs.bvh[0].shapes.size(); ++i) {
+            const Quat q = load_quat(hs.bvh[0].shapes[i].rot);
+            for (uint32_t a = 0; a < 8; ++a) {
+                if ((a & 3u) == 3u) continue;
+                const double sg = (a & 4u) ? 1.0 : -1.0;
+                const uint32_t dim = a & 3u;
+                const V3 n = dim == 0 ? v3(sg, 0.0, 0.0) : dim == 1 ? v3(0.0, sg, 0.0) : v3(0.0, 0.0, sg);
+                store3(&bn[i * 24 + a * 3], normalize(rotate(q, n)));
+            }
+        }
+        if ((rc = upload(s, pn, &d.plane_nrm)) || (rc = upload(s, bn, &d.box_nrm))) {
+            free_scene(s);
+            return rc;
+        }
+    }
     d.n_lights = d.lboxes.n_prims + d.lells.n_prims + d.ltris.n_prims;
     // UINT64_MAX - (2^64 - n) % n (oracle.c usize_zone); unused without lights
     d.light_zone = d.n_lights ? UINT64_MAX - (0ull - (uint64_t)d.n_lights) % (uint64_t)d.n_lights : 0;

@@ -380,10 +380,13 @@ RT_D bool bvh_closest_sel(const DevBvh& B, bool rfast, V3 o, V3 d, const Rcp3& r
     return bvh_closest<KIND, ST, false>(B, o, d, rc, S, C, bt_out, bu, bv, bprim, baux);
 }
 
-// Materialise the winning candidate (model-space normals) + its rotation.
-RT_D Hit materialise(const DevScene& S, const Cand& c, V3 o, V3 d, Quat& rot, uint32_t& mat, int32_t& gid) {
+// Materialise the winning candidate: model-space normals + their rotation, or
+// (world = true) the final world normals.
+RT_D Hit materialise(const DevScene& S, const Cand& c, V3 o, V3 d, Quat& rot, uint32_t& mat, int32_t& gid,
+                     bool& world) {
     Hit h;
     h.t = c.t;
+    world = false;
     if (c.kind == 3) {  // Triangle::intersection tail (triangle.rs:71-79), DONT_ROTATE
         const DevBvh& B = S.tris;
         const DevTriCold& tc = B.tri_cold[c.prim];
@@ -398,21 +401,28 @@ RT_D Hit materialise(const DevScene& S, const Cand& c, V3 o, V3 d, Quat& rot, ui
         gid = B.gid[c.prim];
         return h;
     }
-    const DevShape* sp;
-    if (c.kind == 0) { sp = &S.planes[c.prim]; mat = S.plane_mat[c.prim]; gid = S.plane_gid[c.prim]; }
-    else {
-        const DevBvh& B = c.kind == 1 ? S.boxes : S.ells;
-        sp = &B.shapes[c.prim]; mat = B.mat[c.prim]; gid = B.gid[c.prim];
-    }
-    const DevShape s = *sp;
-    rot = load_quat(s.rot);
-    if (c.kind == 0) {
-        V3 n = load3(s.shape) * ((c.aux & 1u) ? 1.0 : -1.0);
+    // Plane sides and box faces have per-primitive constant normals: their
+    // with_rotated_normal result (rotate by rot, normalize) is a host-computed
+    // table (DevScene::plane_nrm / box_nrm), so `world` skips rotated().
+    if (c.kind == 0) {  // n * (aux bit0 ? 1 : -1)
+        mat = S.plane_mat[c.prim]; gid = S.plane_gid[c.prim];
+        const V3 n = load3(S.plane_nrm + ((size_t)c.prim * 2 + (c.aux & 1u)) * 3);
         h.ng = n; h.ns = n; h.inside = false;
-    } else if (c.kind == 1) {
-        V3 n = aux_box_normal(c.aux);
+        world = true;
+        return h;
+    }
+    if (c.kind == 1) {  // aux_box_normal(aux)
+        mat = S.boxes.mat[c.prim]; gid = S.boxes.gid[c.prim];
+        const V3 n = load3(S.box_nrm + ((size_t)c.prim * 8 + (c.aux & 7u)) * 3);
         h.ng = n; h.ns = n; h.inside = (c.aux & 8u) != 0;
-    } else {
+        world = true;
+        return h;
+    }
+    const DevBvh& B = S.ells;
+    mat = B.mat[c.prim]; gid = B.gid[c.prim];
+    const DevShape s = B.shapes[c.prim];
+    rot = load_quat(s.rot);
+    {
         V3 mo, md;
         model_ray(s, o, d, mo, md);
         V3 n = ell_normal(load_radii(s), mo, md, c.t);
@@ -468,8 +478,9 @@ RT_D bool intersect_tail(const DevScene& S, const Cand& best, V3 o, V3 d, Cnt<ST
     if (!(best.t * magnitude(d) <= INFINITY)) return false;  // :56
     const unsigned long long ph = PH_T();
     Quat rot;
-    Hit h = materialise(S, best, o, d, rot, mat, gid);
-    out = rotated(h, rot);
+    bool world;
+    Hit h = materialise(S, best, o, d, rot, mat, gid, world);
+    out = world ? h : rotated(h, rot);
     PH_ADD(kPhMaterialise, ph);
     C.shaded();
     return true;

@@ -87,6 +87,11 @@ struct DevScene {
     DevBvh lboxes, lells, ltris;       // LightPrimitives (scene.rs:64-69)
     const DevMaterial* mats;
     uint32_t max_depth;                // max BVH depth over the six (stack bound)
+    // with_rotated_normal (intersections.rs:32-39) of the per-primitive constant
+    // normals, computed on the host with the device's ops: plane [n][side][3]
+    // (side = aux bit0), box in BVH order [n][aux & 7][3] (face dim, sign bit)
+    const double* plane_nrm;
+    const double* box_nrm;
 };
 
 }  // namespace rt
