@@ -60,7 +60,10 @@ struct PathWork {
     uint32_t* spill_n;    // traversal-stack spill, stride grid*64
     double* spill_t;
 };
-constexpr uint32_t kRingRows = 8;   // render.hip kRing
+#ifndef RT_RING_ROWS
+#define RT_RING_ROWS 8
+#endif
+constexpr uint32_t kRingRows = RT_RING_ROWS;   // render.hip kRing (power of two, <= 64)
 constexpr uint64_t kDeepSceneNodes = 4096;  // BVH nodes above which the 4-wave kernel runs
 constexpr size_t kQueueWords = 16;  // wave-tile counter (word 0), padded to a 64-B line
 
