@@ -8,7 +8,8 @@
 //                        take (sample, pixel) paths dynamically and commit
 //                        radiance per pixel in sample order.
 //   reduce_chunks_kernel chunk partial sums -> per-pixel mean
-//   intersect_kernel     batch `intersect` (intersections.rs:42-62)
+//   intersect_kernel     batch `intersect` (intersections.rs:42-62), one thread per ray
+//   trace_kernel         the same, persistent: waves refill finished lanes from a queue
 //   light_kernel         batch intersect_lights / Light::pdf
 //                        (intersections.rs:87-91, ray_sampler.rs:132-139)
 //   unpack_kernel        gathered tiles -> row-major image
@@ -848,7 +849,9 @@ RT_D void wave_flush(const Cnt<ST>& C, unsigned long long* stats, uint32_t wave_
 constexpr int kRing = (int)kRingRows;
 
 // WAVES = minimum waves per SIMD the register budget must allow (3: 168 VGPRs,
-// 4: 128 VGPRs + spill); chosen per scene by the host.
+// 4: 128 VGPRs + spill); RES = the resumable segment form (segment_begin /
+// suspendable trav_step / segment_end) instead of the fused `segment`; both
+// chosen per scene by the host.
 //
 // The scene and frame constants come by pointer (device memory), and each loop
 // trip re-derives the pointers through opaque(): their fields are then
