@@ -20,6 +20,7 @@ and "cpu_baseline" (the oracle, the C restatement of the reference, timed on
 a bounded row window of the same frame on the host cores; rank 0, N=1 only).
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -158,6 +159,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc child passes (traffic=null)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (RCCL over xGMI, the product path); gloo gathers host copies and lets several "
+                         "ranks share one GPU (a rehearsal of the N>1 path on a one-GPU box)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -166,10 +170,14 @@ def main():
     traffic, traffic_detail = None, "not collected (N>1 or --no-pmc)"
     if world == 1 and not args.no_pmc:  # before this process touches the GPU
         traffic, traffic_detail = pmc_traffic(args)
+    local = local % max(1, torch.cuda.device_count())  # > 1 rank per GPU only in a gloo rehearsal
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
     rt = load_package()
 
     scene_file, W, H, spp, depth = WORKLOADS[args.workload]
@@ -209,7 +217,14 @@ def main():
         if timed:
             e1.record(stream)
             ev.append((e0, e1))
-        src = rt.gather_tiles(tiles, gathered, rank, world)
+        if args.dist_backend == "nccl" or world == 1:
+            src = rt.gather_tiles(tiles, gathered, rank, world)
+        else:  # gloo: the same single gather on host copies
+            g_host = torch.empty(gathered.shape, dtype=gathered.dtype) if rank == 0 else None
+            rt.gather_tiles(tiles.cpu(), g_host, rank, world)
+            if rank == 0:
+                gathered.copy_(g_host)
+            src = gathered
         if rank == 0:
             rt.unpack_tiles_bytes_async(params, world, src.data_ptr(), image.data_ptr(), sptr)
 
@@ -253,7 +268,8 @@ def main():
                 "triangles": int(len(desc.tri_material)), "shapes": int(len(desc.shapes)),
                 "width": W, "height": H, "spp": spp, "ray_depth": params.ray_depth,
                 "paths_per_step": frame_paths, "segments_per_step": frame_segments,
-                "parallelism": f"tiles16x16 round-robin over {world} GPU(s) + 1 RCCL gather",
+                "parallelism": f"tiles16x16 round-robin over {world} rank(s) + 1 "
+                               f"{'RCCL' if args.dist_backend == 'nccl' else 'gloo (rehearsal)'} gather",
                 "epilogue": "device unpack + ACES + gamma + PPM bytes (rt_unpack_tiles_bytes_async)",
                 "seed": params.seed,
             },
@@ -280,6 +296,8 @@ def main():
         elif world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(desc, params, args.cpu_seconds)
             out["speedup_vs_cpu"] = value / out["cpu_baseline"]["value"]
+        # the PPM payload of the last frame (outside the timed region): identical for any N
+        out["image_sha256"] = hashlib.sha256(image.cpu().numpy().tobytes()).hexdigest()
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
