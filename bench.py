@@ -126,24 +126,34 @@ def cpu_baseline(desc, params, target_s):
     import oracle as orc
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     osc = orc.OracleScene(desc)
+    # grow a centred band of rows in small slices until ~target_s of CPU work is
+    # done (the box's CPU share varies, so a one-shot calibration over- or
+    # under-shoots by several x); the rate is segments / time over all slices
     mid = params.height // 2
-    # calibrate on 2 rows, then size the window for ~target_s of CPU work
-    t = time.perf_counter()
-    _, _, st = osc.render(params, mode=0, threads=threads, rows=(mid, mid + 2))
-    dt = time.perf_counter() - t
-    rows = int(max(2, min(params.height, 2 * target_s / max(dt, 1e-3))))
-    r0 = max(0, mid - rows // 2)
-    r1 = min(params.height, r0 + rows)
-    t = time.perf_counter()
-    _, _, st = osc.render(params, mode=0, threads=threads, rows=(r0, r1))
-    dt = time.perf_counter() - t
+    r0 = r1 = mid
+    segs = paths = 0
+    dt = 0.0
+    step = 2
+    while dt < target_s and (r0 > 0 or r1 < params.height):
+        lo, hi = max(0, r0 - step // 2), min(params.height, r1 + step - step // 2)
+        for a, b in ((lo, r0), (r1, hi)):
+            if b <= a:
+                continue
+            t = time.perf_counter()
+            _, _, st = osc.render(params, mode=0, threads=threads, rows=(a, b))
+            dt += time.perf_counter() - t
+            segs += st["segments"]
+            paths += st["paths"]
+        r0, r1 = lo, hi
+        rate = (r1 - r0) / max(dt, 1e-3)  # rows per second so far
+        step = int(max(2, min(2 * (r1 - r0), rate * (target_s - dt) / 2)))
     return {
-        "value": st["segments"] / dt / 1e6,
+        "value": segs / dt / 1e6,
         "unit": "Msamples/s",
         "cores": threads,
         "kind": "port",
         "sample": f"rows {r0}..{r1} of {params.width}x{params.height} at {params.spp} spp "
-                  f"({st['paths']} paths, {st['segments']} segments, {dt:.1f} s), recursive raytrace_impl, "
+                  f"({paths} paths, {segs} segments, {dt:.1f} s), recursive raytrace_impl, "
                   f"OpenMP dynamic over pixels",
         "seconds": dt,
     }
