@@ -110,10 +110,52 @@ struct Cand {
     bool valid;
 };
 
-// closest hit of one shape in model space; t + aux
+// Plane::intersection for a kPlaneAxis plane (n = sign * e_K) and a ray_fast
+// ray, when o[K] - pos[K] != 0: then model_ray's mo[K] and md[K] are o[K] -
+// pos[K] and d[K] bit for bit (finite operands, identity rotation), n.mo =
+// sign * x and n.d = sign * d[K] exactly (the zero terms add signed zeros to a
+// nonzero value), so t = -(sign x) / (sign d[K]) = -RN(x / d[K]) — by
+// fdiv_fast, exact for x in [2^-449, 2^401] (shape_fast).  Returns -1 when the
+// lane must take the generic form (x == 0), else hit (1) / miss (0).
+template <int K>
+RT_D int plane_axis_t(const DevShape& s, V3 o, V3 d, const Rcp3& rc, double& t, uint32_t& aux) {
+    const double x = comp(o, K) - s.pos[K];
+    if (x == 0.0) return -1;
+    const double dk = comp(d, K);
+    const double tt = -fdiv_fast(x, dk, comp(rc.r, K));
+    if (tt < 0.0) return 0;
+    t = tt;
+    aux = ((s.axis & 4u) ? -dk : dk) <= 0.0 ? 1u : 0u;
+    return 1;
+}
+
+// closest hit of one shape in model space; t + aux.  rfast: the ray passed
+// ray_fast (kShapeFast shapes may then take the exact unguarded division).
 template <int KIND>
-RT_D bool shape_closest(const DevShape& s, V3 o, V3 d, const Rcp3& rc, double& t, uint32_t& aux) {
+RT_D bool shape_closest(const DevShape& s, V3 o, V3 d, const Rcp3& rc, bool rfast, double& t, uint32_t& aux) {
     V3 mo, md;
+#ifndef RT_NO_FASTSHAPE  // ablation build: the generic form for every shape
+    if (KIND == 0 && rfast && (s.flags & (kShapeFast | kPlaneAxis)) == (kShapeFast | kPlaneAxis)) {
+        const uint32_t k = s.axis & 3u;  // uniform: one scalar branch
+        const int r = k == 0 ? plane_axis_t<0>(s, o, d, rc, t, aux)
+                    : (k == 1 ? plane_axis_t<1>(s, o, d, rc, t, aux) : plane_axis_t<2>(s, o, d, rc, t, aux));
+        if (r >= 0) return r != 0;
+    }
+    if (KIND != 0 && shape_fast(s, rfast, o, mo)) {
+        if (KIND == 1) {
+            Bpi en, ex;
+            int k = box_coef<true>(load3(s.shape), mo, d, rc, en, ex);
+            if (k == 2) { t = en.t; aux = bpi_aux(en, false); return true; }
+            if (k == 1) { t = ex.t; aux = bpi_aux(ex, true); return true; }
+            return false;
+        }
+        double t1, t2;
+        int k = ell_coef<true>(load_radii(s), mo, d, t1, t2);
+        if (k == 2) { t = t1; aux = 0; return true; }
+        if (k == 1) { t = t2; aux = 8; return true; }
+        return false;
+    }
+#endif
     const bool same = model_ray(s, o, d, mo, md);
     if (KIND == 0) return plane_t(load3(s.shape), mo, md, t, aux);
     if (KIND == 1) {
@@ -198,7 +240,7 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
                 uint32_t aux = 0;
                 bool h;
                 if (KIND == 3) { C.tri(); h = tri_uvt(B.tris[i], o, d, u, v, t); }
-                else { C.shape(); h = shape_closest<KIND>(B.shapes[i], o, d, rc, t, aux); }
+                else { C.shape(); h = shape_closest<KIND>(B.shapes[i], o, d, rc, fast, t, aux); }
                 if (h && (!T.valid || t < T.best)) {  // update_best_intersection (bvh.rs:213-222)
                     T.valid = true; T.best = t; T.bu = u; T.bv = v; T.prim = i; T.aux = aux;
                 }
@@ -283,7 +325,7 @@ RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stk& S, Cnt<S
             uint32_t aux = 0;
             bool h;
             if (KIND == 3) { C.tri(); h = tri_uvt(B.tris[i], o, d, u, v, t); }
-            else { C.shape(); h = shape_closest<KIND>(B.shapes[i], o, d, rc, t, aux); }
+            else { C.shape(); h = shape_closest<KIND>(B.shapes[i], o, d, rc, FAST, t, aux); }
             if (h && (!valid || t < best)) {  // update_best_intersection (bvh.rs:213-222)
                 valid = true; best = t; bu = u; bv = v; bprim = i; baux = aux;
             }
@@ -317,7 +359,7 @@ RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stk& S, Cnt<S
                     uint32_t aux = 0;
                     bool h;
                     if (KIND == 3) { C.tri(); h = tri_uvt(B.tris[i], o, d, u, v, t); }
-                    else { C.shape(); h = shape_closest<KIND>(B.shapes[i], o, d, rc, t, aux); }
+                    else { C.shape(); h = shape_closest<KIND>(B.shapes[i], o, d, rc, FAST, t, aux); }
                     if (h && (!valid || t < best)) {  // update_best_intersection (bvh.rs:213-222)
                         valid = true; best = t; bu = u; bv = v; bprim = i; baux = aux;
                     }
@@ -446,7 +488,7 @@ RT_D void shapes_closest(const DevScene& S, V3 o, V3 d, const Rcp3& rc, bool rfa
     for (uint32_t i = 0; i < S.n_planes; ++i) {  // :45-49
         double t; uint32_t aux;
         C.shape();
-        if (!shape_closest<0>(S.planes[i], o, d, rc, t, aux)) continue;
+        if (!shape_closest<0>(S.planes[i], o, d, rc, rfast, t, aux)) continue;
         if (!best.valid || t < best.t) { best.valid = true; best.t = t; best.prim = i; best.aux = aux; best.kind = 0; }
     }
     PH_ADD(kPhPlanes, ph);
@@ -512,8 +554,8 @@ RT_D double prob_ell(V3 r, V3 ng) {
 // the Light::pdf callback over the primitives [start, start + cnt) of a leaf
 // (bvh.rs:194-198 -> intersection_probability.rs:9-35)
 template <int KIND, bool ST>
-RT_D void leaf_all(const DevBvh& B, uint32_t start, uint32_t cnt, V3 o, V3 d, const Rcp3& rc, Cnt<ST>& C,
-                   double& impact, uint32_t& nhits) {
+RT_D void leaf_all(const DevBvh& B, uint32_t start, uint32_t cnt, V3 o, V3 d, const Rcp3& rc, bool rfast,
+                   Cnt<ST>& C, double& impact, uint32_t& nhits) {
     for (uint32_t i = start; i < start + cnt; ++i) {
         if (KIND == 3) {
             C.tri();
@@ -527,13 +569,21 @@ RT_D void leaf_all(const DevBvh& B, uint32_t start, uint32_t cnt, V3 o, V3 d, co
             C.shape();
             const DevShape s = B.shapes[i];
             V3 mo, md;
-            const bool same = model_ray(s, o, d, mo, md);
+#ifndef RT_NO_FASTSHAPE
+            const bool fs = shape_fast(s, rfast, o, mo);  // then model_ray gives (o - pos, d)
+#else
+            const bool fs = false;
+#endif
+            bool same = true;
+            if (fs) md = d;
+            else same = model_ray(s, o, d, mo, md);
             Quat q = load_quat(s.rot);
             const bool qid = is_identity(q);
             V3 sz = load3(s.shape);
             if (KIND == 1) {
                 Bpi en, ex;
-                int k = box_coef(sz, mo, md, same ? rc : make_rcp3(md), en, ex);
+                int k = fs ? box_coef<true>(sz, mo, md, rc, en, ex)
+                           : box_coef(sz, mo, md, same ? rc : make_rcp3(md), en, ex);
                 const double pb = s.aux[0];
                 // |d . normalize(rotate(q, n))| for a face normal n = sign * e_dim.  With an
                 // identity q, rotate returns n up to the signs of its zero components and
@@ -552,7 +602,7 @@ RT_D void leaf_all(const DevBvh& B, uint32_t start, uint32_t cnt, V3 o, V3 d, co
             } else {
                 double t1, t2;
                 const Radii R = load_radii(s);
-                int k = ell_coef(R, mo, md, t1, t2);
+                int k = fs ? ell_coef<true>(R, mo, md, t1, t2) : ell_coef(R, mo, md, t1, t2);
                 if (k == 2) {
                     V3 ng = normalize(rotate_fast(q, qid, ell_normal(R, mo, md, t1)));
                     impact += prob_ell(sz, ng) * (t1 * t1 / fabs(dot(d, ng)));
@@ -570,14 +620,15 @@ RT_D void leaf_all(const DevBvh& B, uint32_t start, uint32_t cnt, V3 o, V3 d, co
 
 // Node::intersections (bvh.rs:188-210) accumulating the Light::pdf callback
 template <int KIND, bool ST, class Stk>
-RT_D void bvh_all(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stk& S, Cnt<ST>& C, double& impact,
+RT_D void bvh_all(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool rfast, Stk& S, Cnt<ST>& C, double& impact,
                   uint32_t& nhits) {
     if (B.n_prims == 0) return;
     double t0;
     C.aabb();
-    if (!aabb_hit(load3(B.root_min), load3(B.root_max), o, d, rc, t0)) return;
+    const bool fast = B.fast && rfast;  // unguarded exact slab division (aabb_hit_fast)
+    if (!slab<2>(B.root_min, B.root_max, o, d, rc, fast, t0)) return;
     if (B.depth == 1) {  // the root is the only leaf: [0, n_prims), no stack
-        leaf_all<KIND, ST>(B, 0u, B.n_prims, o, d, rc, C, impact, nhits);
+        leaf_all<KIND, ST>(B, 0u, B.n_prims, o, d, rc, rfast, C, impact, nhits);
         return;
     }
     uint32_t node = 0;
@@ -585,13 +636,13 @@ RT_D void bvh_all(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stk& S, Cnt<ST>& 
     for (;;) {
         const DevNode& n = B.nodes[node];
         const uint32_t cnt = n.count, start = n.start;
-        leaf_all<KIND, ST>(B, start, cnt, o, d, rc, C, impact, nhits);
+        leaf_all<KIND, ST>(B, start, cnt, o, d, rc, rfast, C, impact, nhits);
         const int32_t left = n.left;
         if (left >= 0) {
             double lt, rt2;
             C.aabb(2);
-            bool lh = aabb_hit(load3(n.lmin), load3(n.lmax), o, d, rc, lt);
-            bool rh = aabb_hit(load3(n.rmin), load3(n.rmax), o, d, rc, rt2);
+            bool lh = slab<2>(n.lmin, n.lmax, o, d, rc, fast, lt);
+            bool rh = slab<2>(n.rmin, n.rmax, o, d, rc, fast, rt2);
             if (lh) {
                 if (rh) S.push((uint32_t)n.right, 0.0);
                 node = (uint32_t)left;
@@ -609,10 +660,11 @@ RT_D void bvh_all(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stk& S, Cnt<ST>& 
 template <bool ST, class Stk>
 RT_D double lights_impact(const DevScene& S, V3 o, V3 d, Stk& stk, Cnt<ST>& C, uint32_t& nhits) {
     double impact = 0.0;
-    const Rcp3 rc = make_rcp3(d);  // dead (DCE'd) unless RT_FASTDIV
-    bvh_all<1, ST>(S.lboxes, o, d, rc, stk, C, impact, nhits);
-    bvh_all<2, ST>(S.lells, o, d, rc, stk, C, impact, nhits);
-    bvh_all<3, ST>(S.ltris, o, d, rc, stk, C, impact, nhits);
+    const Rcp3 rc = make_rcp3(d);
+    const bool rfast = ray_fast(o, rc);
+    bvh_all<1, ST>(S.lboxes, o, d, rc, rfast, stk, C, impact, nhits);
+    bvh_all<2, ST>(S.lells, o, d, rc, rfast, stk, C, impact, nhits);
+    bvh_all<3, ST>(S.ltris, o, d, rc, rfast, stk, C, impact, nhits);
     return impact;
 }
 template <bool ST, class Stk>

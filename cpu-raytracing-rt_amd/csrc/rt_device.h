@@ -198,6 +198,12 @@ RT_D double fdiv_fast(double x, double y, double r) {
     const double e1 = fma(-q1, y, x);
     return fma(e1, r, q1);
 }
+// fdiv_fast that also returns x / y's signed zero for x == +-0 (x * r has the
+// sign sign(x) ^ sign(y), as x / y does): exact for every x in the range.
+RT_D double fdiv_fastz(double x, double y, double r) {
+    const double q = fdiv_fast(x, y, r);
+    return x == 0.0 ? x * r : q;
+}
 constexpr double kInvPi = 1.0 / kPi;  // RN(1/pi), folded exactly at compile time
 RT_D double div_pi(double x) { return fdiv_r(x, kPi, kInvPi, true); }
 
@@ -318,6 +324,18 @@ RT_D bool model_ray(const DevShape& s, V3 o, V3 d, V3& mo, V3& md) {
     return same;
 }
 
+// Model-space origin of a ray_fast ray for a kShapeFast shape (identity
+// rotation, rt_layout.h) when it equals model_ray's bit for bit: o - pos and d
+// without zero components, which rotate_fast returns unchanged (md = d).  Then
+// o, pos and the shape's sizes are 0 or multiples of 2^-449 below 2^401, so
+// every quotient of the box/ellipsoid test has a dividend that is 0 or in
+// [2^-449, 2^402] and takes fdiv_fast(z) exactly.
+RT_D bool shape_fast(const DevShape& s, bool rfast, V3 o, V3& mo) {
+    if (!rfast || !(s.flags & kShapeFast)) return false;
+    mo = o - load3(s.pos);
+    return mo.x != 0.0 && mo.y != 0.0 && mo.z != 0.0;
+}
+
 // Plane::intersection (plane.rs:11-21); aux bit0 = (nd <= 0)
 RT_D bool plane_t(V3 n, V3 o, V3 d, double& t, uint32_t& aux) {
     double nd = dot(n, d);
@@ -330,16 +348,19 @@ RT_D bool plane_t(V3 n, V3 o, V3 d, double& t, uint32_t& aux) {
 
 // intersect_box_coef (box.rs:75-115). Entry/exit as (t, sign, dim).
 struct Bpi { double t; double sign; int dim; };
+// FD: shape_fast holds (d has no zero component; every quotient exact by fdiv_fastz)
+template <bool FD = false>
 RT_D int box_coef(V3 s, V3 o, V3 d, const Rcp3& rc, Bpi& en, Bpi& ex) {
     bool have = false;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         double di = comp(d, i), oi = comp(o, i), si = comp(s, i);
-        if (di == 0.0 && si < fabs(oi)) return 0;
-        if (di == 0.0) continue;
+        if (!FD && di == 0.0 && si < fabs(oi)) return 0;
+        if (!FD && di == 0.0) continue;
         const double ri = comp(rc.r, i);
         const bool ok = (rc.ok >> i) & 1u;
-        double t1 = fdiv_r(si - oi, di, ri, ok), t2 = fdiv_r(-si - oi, di, ri, ok);
+        double t1 = FD ? fdiv_fastz(si - oi, di, ri) : fdiv_r(si - oi, di, ri, ok);
+        double t2 = FD ? fdiv_fastz(-si - oi, di, ri) : fdiv_r(-si - oi, di, ri, ok);
         double a, b, nrm;
         if (t1 < t2) { a = t1; b = t2; nrm = 1.0; } else { a = t2; b = t1; nrm = -1.0; }
         if (!have) { en = Bpi{a, nrm, i}; ex = Bpi{b, nrm, i}; have = true; }
@@ -385,9 +406,17 @@ RT_D V3 div_radii(V3 v, const Radii& R) {  // v.div_element_wise(r)
               fdiv_r(v.z, R.r.z, R.inv.z, R.ok & 4u));
 }
 
-// intersect_ellipsoid_coef (ellipsoid.rs:49-76)
+// intersect_ellipsoid_coef (ellipsoid.rs:49-76).  FD: shape_fast holds (o
+// and d without zero components, radii fd_ok: o / r and d / r by fdiv_fast)
+template <bool FD = false>
 RT_D int ell_coef(const Radii& R, V3 o, V3 d, double& t1o, double& t2o) {
-    V3 oo = div_radii(o, R), dd = div_radii(d, R);
+    V3 oo, dd;
+    if (FD) {
+        oo = v3(fdiv_fast(o.x, R.r.x, R.inv.x), fdiv_fast(o.y, R.r.y, R.inv.y), fdiv_fast(o.z, R.r.z, R.inv.z));
+        dd = v3(fdiv_fast(d.x, R.r.x, R.inv.x), fdiv_fast(d.y, R.r.y, R.inv.y), fdiv_fast(d.z, R.r.z, R.inv.z));
+    } else {
+        oo = div_radii(o, R); dd = div_radii(d, R);
+    }
     double c = dot(oo, oo), b = dot(oo, dd), a = dot(dd, dd);
     double disc = b * b - a * (c - 1.0);
     if (disc < 0.0) return 0;

@@ -40,8 +40,14 @@ struct alignas(16) DevShape {  // Primitive<T> hot part (scene.rs:20-27)
     //   ellipsoid: aux = RN(1/r) per axis (exact reciprocal division, RT_FASTDIV)
     //   box:       aux[0] = 1/sum/8 (intersection_probability.rs:15-23)
     double aux[3];
-    double pad;
+    // kShapeFast: identity rotation, position (and box sizes / plane normal /
+    // ellipsoid radii) in coord_fast range, nonzero box sizes, fd_ok radii —
+    // a ray_fast ray may then take fdiv_fast for this shape's quotients
+    // (rt_device.h shape_fast).  kPlaneAxis: plane normal = sign * e_axis.
+    uint32_t flags;
+    uint32_t axis;             // plane: 0..2, bit 2 = negative sign
 };
+constexpr uint32_t kShapeFast = 1u, kPlaneAxis = 2u;
 static_assert(sizeof(DevShape) == 112, "shape record");
 
 struct alignas(16) DevTri {    // Triangle hot part (triangle.rs:5-17)

@@ -253,6 +253,38 @@ void flatten(const HostBvh& h, HostBvhArrays& out) {
     out.fast = fast;
 }
 
+// rt_device.h fd_ok on the host: |v| in [2^-450, 2^451)
+static bool fd_ok_host(double v) {
+    uint64_t b;
+    std::memcpy(&b, &v, sizeof b);
+    return ((uint32_t)(b >> 52) & 0x7ffu) - 573u < 901u;
+}
+// DevShape::flags (rt_layout.h): which shapes a ray_fast ray may test with the
+// unguarded exact division, and planes whose normal is a signed axis
+static uint32_t shape_flags(const rt_shape& s, uint32_t& axis) {
+    axis = 0;
+    const double* q = s.rotation;  // (s, x, y, z)
+    bool fast = q[0] == 1.0 && q[1] == 0.0 && q[2] == 0.0 && q[3] == 0.0;
+    for (int k = 0; k < 3; ++k) fast = fast && coord_fast(s.position[k]);
+    uint32_t f = 0;
+    if (s.type == RT_SHAPE_BOX)
+        for (int k = 0; k < 3; ++k) fast = fast && coord_fast(s.shape[k]) && s.shape[k] != 0.0;
+    if (s.type == RT_SHAPE_ELLIPSOID)
+        for (int k = 0; k < 3; ++k) fast = fast && fd_ok_host(s.shape[k]);
+    if (s.type == RT_SHAPE_PLANE) {
+        int zeros = 0, k1 = -1;
+        for (int k = 0; k < 3; ++k) {
+            if (s.shape[k] == 0.0) zeros++;
+            else if (s.shape[k] == 1.0 || s.shape[k] == -1.0) k1 = k;
+        }
+        if (zeros == 2 && k1 >= 0) {
+            f |= kPlaneAxis;
+            axis = (uint32_t)k1 | (s.shape[k1] < 0.0 ? 4u : 0u);
+        }
+    }
+    return f | (fast ? kShapeFast : 0u);
+}
+
 struct ShapeItem { DevShape s; uint32_t mat; int32_t gid; Box3 box; };
 struct TriItem { Triangle t; uint32_t mat; int32_t gid; Box3 box; };
 
@@ -369,6 +401,7 @@ std::string build_scene(const rt_scene_desc& d, HostScene& out) {
             const double* z = s.shape;
             it.s.aux[0] = 1.0 / ((z[1] * z[2] + z[0] * z[2]) + z[0] * z[1]) / 8.0;
         }
+        it.s.flags = shape_flags(s, it.s.axis);
         it.mat = s.material;
         it.gid = (int32_t)i;
         if (s.type == RT_SHAPE_PLANE) {  // Primitive::new_without_aabb (scene.rs:126-136)

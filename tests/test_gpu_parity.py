@@ -304,3 +304,81 @@ def test_deep_stack_and_big_leaf(rt, orc):
 def _tri_boxes(desc):
     v = desc.tri_vertices.reshape(-1, 3, 3)
     return np.concatenate([v.min(1), v.max(1)], axis=1)
+
+
+AXIS_SCENE = """DIMENSIONS 24 20
+SAMPLES 3
+RAY_DEPTH 8
+BG_COLOR 0.1 0.1 0.1
+CAMERA_POSITION 0 0 -2
+NEW_PRIMITIVE
+PLANE 0 1 0
+POSITION 0 -1 0
+COLOR 0.7 0.7 0.7
+NEW_PRIMITIVE
+PLANE 0 0 -1
+POSITION 0 0 1
+COLOR 0.6 0.6 0.6
+NEW_PRIMITIVE
+PLANE -1 0 0
+POSITION 1 0 0
+COLOR 0.2 0.8 0.2
+NEW_PRIMITIVE
+PLANE 1 0 0
+POSITION -1 0 0
+COLOR 0.8 0.2 0.2
+NEW_PRIMITIVE
+PLANE 0 -2 0
+POSITION 0 1 0
+COLOR 0.5 0.5 0.5
+NEW_PRIMITIVE
+BOX 0.25 0.5 0.25
+POSITION 0.25 -0.5 0.5
+COLOR 0.8 0.8 0.8
+NEW_PRIMITIVE
+BOX 0.25 0.125 0.25
+POSITION 0 0.875 0
+EMISSION 5 5 5
+NEW_PRIMITIVE
+ELLIPSOID 0.25 0.5 0.375
+POSITION -0.5 0 0.25
+EMISSION 2 3 4
+COLOR 0.3 0.3 0.3
+NEW_PRIMITIVE
+ELLIPSOID 0.25 0.25 0.25
+POSITION 0.5 0.25 -0.25
+COLOR 1 1 1
+DIELECTRIC
+IOR 1.5
+"""
+
+
+def test_fast_shape_edges(rt, orc):
+    """Identity-rotation shapes and signed-axis planes take the exact unguarded
+    division for ray_fast rays (rt_device.h shape_fast, plane_axis_t).  Dyadic
+    origins put o - pos on exact zeros (generic fallback lanes), origins on box
+    faces (signed-zero quotients), zero direction components (no fast ray) and
+    a non-unit axis normal (generic plane): hits, raw light sums and pdfs must
+    equal the oracle's bit for bit, incl. the signs of zeros."""
+    desc, params = rt.parse_scene(AXIS_SCENE)
+    g, o = rt.Scene(desc), orc.OracleScene(desc)
+    rng = np.random.default_rng(21)
+    n = 40000
+    orig = rng.integers(-8, 9, (n, 3)) / 8.0             # on the shapes' dyadic grid
+    orig[n // 2:] += rng.uniform(-1e-3, 1e-3, (n - n // 2, 3)) * (rng.random((n - n // 2, 3)) < 0.5)
+    d = rng.standard_normal((n, 3))
+    d[:2000, 0] = 0.0
+    d[2000:4000] = rng.integers(-2, 3, (2000, 3)) / 2.0  # axis and diagonal directions, some zero
+    d[2000:4000][np.all(d[2000:4000] == 0, axis=1)] = [0.0, 1.0, 0.0]
+    rays = np.concatenate([orig, d], axis=1)
+    gh, oh = g.intersect(rays), o.intersect(rays)
+    assert np.array_equal(gh.view(np.uint8), oh.view(np.uint8))
+    assert (gh["prim"] >= 0).sum() > n // 2
+    gi, gc = g.intersect_lights(rays)
+    oi, oc = o.intersect_lights(rays)
+    assert np.array_equal(gc, oc) and gc.sum() > 1000
+    assert np.array_equal(gi.view(np.uint64), oi.view(np.uint64))
+    dn = d / np.linalg.norm(d, axis=1, keepdims=True)
+    pd = np.concatenate([orig, dn], axis=1)
+    assert np.array_equal(g.light_pdf(pd).view(np.uint64), o.light_pdf(pd).view(np.uint64))
+    _compare(g, o, params)
