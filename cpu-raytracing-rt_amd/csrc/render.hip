@@ -320,12 +320,21 @@ RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stk& S, Cnt<S
     bool valid = false;
     double best = INFINITY;
     if (B.depth == 1) {  // the root is the only leaf (bvh.rs:77, <= 4 primitives): [0, n_prims) in order
-        for (uint32_t i = 0; i < B.n_prims; ++i) {
+#ifndef RT_NO_UNI  // uniform index: the records come through the scalar cache
+        const uint32_t np = uni_u32(B.n_prims);
+        const RT_CAS DevTri* tris = uni(B.tris);
+        const RT_CAS DevShape* shapes = uni(B.shapes);
+#else
+        const uint32_t np = B.n_prims;
+        const DevTri* tris = B.tris;
+        const DevShape* shapes = B.shapes;
+#endif
+        for (uint32_t i = 0; i < np; ++i) {
             double t, u = 0.0, v = 0.0;
             uint32_t aux = 0;
             bool h;
-            if (KIND == 3) { C.tri(); h = tri_uvt(B.tris[i], o, d, u, v, t); }
-            else { C.shape(); h = shape_closest<KIND>(B.shapes[i], o, d, rc, FAST, t, aux); }
+            if (KIND == 3) { C.tri(); const DevTri tr = tris[i]; h = tri_uvt(tr, o, d, u, v, t); }
+            else { C.shape(); const DevShape sh = shapes[i]; h = shape_closest<KIND>(sh, o, d, rc, FAST, t, aux); }
             if (h && (!valid || t < best)) {  // update_best_intersection (bvh.rs:213-222)
                 valid = true; best = t; bu = u; bv = v; bprim = i; baux = aux;
             }
@@ -485,10 +494,18 @@ RT_D void shapes_closest(const DevScene& S, V3 o, V3 d, const Rcp3& rc, bool rfa
                          Cand& best) {
     best.valid = false; best.t = 0.0; best.u = best.v = 0.0; best.prim = 0; best.aux = 0; best.kind = 0;
     unsigned long long ph = PH_T();
-    for (uint32_t i = 0; i < S.n_planes; ++i) {  // :45-49
+#ifndef RT_NO_UNI  // ablation build: per-lane flat loads of the plane records
+    const uint32_t np = uni_u32(S.n_planes);
+    const RT_CAS DevShape* planes = uni(S.planes);
+#else
+    const uint32_t np = S.n_planes;
+    const DevShape* planes = S.planes;
+#endif
+    for (uint32_t i = 0; i < np; ++i) {  // :45-49
         double t; uint32_t aux;
         C.shape();
-        if (!shape_closest<0>(S.planes[i], o, d, rc, rfast, t, aux)) continue;
+        const DevShape sh = planes[i];
+        if (!shape_closest<0>(sh, o, d, rc, rfast, t, aux)) continue;
         if (!best.valid || t < best.t) { best.valid = true; best.t = t; best.prim = i; best.aux = aux; best.kind = 0; }
     }
     PH_ADD(kPhPlanes, ph);
@@ -553,21 +570,34 @@ RT_D double prob_ell(V3 r, V3 ng) {
 
 // the Light::pdf callback over the primitives [start, start + cnt) of a leaf
 // (bvh.rs:194-198 -> intersection_probability.rs:9-35)
-template <int KIND, bool ST>
+// UNI: [start, start + cnt) is the same for every lane (the single-leaf BVH),
+// so the shape records come through the scalar cache (uni)
+template <int KIND, bool ST, bool UNI = false>
 RT_D void leaf_all(const DevBvh& B, uint32_t start, uint32_t cnt, V3 o, V3 d, const Rcp3& rc, bool rfast,
                    Cnt<ST>& C, double& impact, uint32_t& nhits) {
+#ifdef RT_NO_UNI
+    constexpr bool kUni = false;
+#else
+    constexpr bool kUni = UNI;
+#endif
+    if (kUni) cnt = uni_u32(cnt);
     for (uint32_t i = start; i < start + cnt; ++i) {
         if (KIND == 3) {
             C.tri();
             double u, v, t;
-            if (tri_uvt(B.tris[i], o, d, u, v, t)) {
+            DevTri tr;
+            if (kUni) tr = uni(B.tris)[i];
+            else tr = B.tris[i];
+            if (tri_uvt(tr, o, d, u, v, t)) {
                 V3 ng = load3(B.tri_cold[i].ng);  // sign flip (triangle.rs:76) cancels in |d.n|
                 impact += B.tri_inv_area[i] * (t * t / fabs(dot(d, ng)));
                 C.lhit(); nhits++;
             }
         } else {
             C.shape();
-            const DevShape s = B.shapes[i];
+            DevShape s;
+            if (kUni) s = uni(B.shapes)[i];
+            else s = B.shapes[i];
             V3 mo, md;
 #ifndef RT_NO_FASTSHAPE
             const bool fs = shape_fast(s, rfast, o, mo);  // then model_ray gives (o - pos, d)
@@ -628,7 +658,7 @@ RT_D void bvh_all(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool rfast, Stk& 
     const bool fast = B.fast && rfast;  // unguarded exact slab division (aabb_hit_fast)
     if (!slab<2>(B.root_min, B.root_max, o, d, rc, fast, t0)) return;
     if (B.depth == 1) {  // the root is the only leaf: [0, n_prims), no stack
-        leaf_all<KIND, ST>(B, 0u, B.n_prims, o, d, rc, rfast, C, impact, nhits);
+        leaf_all<KIND, ST, true>(B, 0u, B.n_prims, o, d, rc, rfast, C, impact, nhits);
         return;
     }
     uint32_t node = 0;

@@ -16,6 +16,28 @@ namespace rt {
 
 #define RT_D __device__ __forceinline__
 
+// Wave-uniform scene data in the scalar path.  The scene's fields reach the
+// kernels through generic pointers, so the compiler reads them with per-lane
+// flat loads (a flat load may hit scratch, so its result counts as divergent)
+// and every dependent access waits a full vector-memory round trip.  A POINTER
+// VALUE read from the scene (device global memory no kernel writes) is made
+// uniform with readfirstlane and viewed in the constant address space: loads
+// through it with a uniform index become s_load through the scalar cache.
+// Only for values every active lane holds (scene pointers and counts).
+#ifdef __HIP_DEVICE_COMPILE__  // the host pass of a .hip file only parses these
+#define RT_CAS __attribute__((address_space(4)))
+#else
+#define RT_CAS
+#endif
+template <class T>
+RT_D const RT_CAS T* uni(const T* p) {
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (const RT_CAS T*)(((uint64_t)hi << 32) | lo);
+}
+RT_D uint32_t uni_u32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
 // ------------------------------------------------------------------ RNG ----
 // Counter-based Philox4x32-10 per (pixel, sample) replaces ThreadRng
 // (main.rs:95); ctr = {block, sample, pixel_lo, pixel_hi}, key = seed.
