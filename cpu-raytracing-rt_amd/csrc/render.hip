@@ -939,10 +939,21 @@ constexpr int kRing = (int)kRingRows;
 // trip re-derives the pointers through opaque(): their fields are then
 // scalar-loaded where used instead of being hoisted into SGPRs for the whole
 // kernel, which (with ~1 KB of them) spilled hundreds of SGPRs into VGPR lanes.
+//
+// The pointer goes through the asm in the constant address space (the scene
+// and frame records are device memory no kernel writes), so the fields are
+// s_load'ed through the scalar cache; as a generic pointer they were per-lane
+// flat loads, each a full vector-memory round trip.
 template <class T>
 RT_D const T* opaque(const T* p) {
+#ifndef RT_FLAT_SCENE  // ablation build: the generic pointer
+    const RT_CAS T* q = (const RT_CAS T*)p;
+    asm volatile("" : "+s"(q));
+    return (const T*)q;
+#else
     asm volatile("" : "+s"(p));
     return p;
+#endif
 }
 
 template <bool ST, bool HIT, int WAVES, bool RES>
@@ -997,11 +1008,17 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
         q.T.live = false;
         bool inq = false;  // this lane's segment query is under way
         for (;;) {
-            // 3 waves: fields scalar-loaded where used (see opaque).  4 waves: the
-            // by-value kernel arguments, which measured faster at its 128-VGPR
-            // budget (C3 2024 vs 2067 ms)
-            const DevScene& S = WAVES == 3 ? *opaque(Sg) : Sv;
-            const KParams& P = WAVES == 3 ? *opaque(Pg) : Pv;
+            // fields s_load'ed where used (see opaque), for both register budgets
+            // (C3 at 64 spp: 315.6 vs 325.9 ms with the by-value kernel
+            // arguments of the 4-wave kernel, whose loads were hoisted into
+            // SGPRs and spilled)
+#ifndef RT_SCENE_BYVAL4  // ablation build: by-value arguments for the 4-wave kernel
+            constexpr bool kByPtr = true;
+#else
+            constexpr bool kByPtr = WAVES == 3;
+#endif
+            const DevScene& S = kByPtr ? *opaque(Sg) : Sv;
+            const KParams& P = kByPtr ? *opaque(Pg) : Pv;
             const Scales sc{P.scale01, P.scale11};
             // hand the next units to idle lanes, in lane order, inside the ring window
             const uint32_t limit = min(total, (base + kRing) * kWave);
