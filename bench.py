@@ -180,7 +180,11 @@ def main():
     traffic, traffic_detail = None, "not collected (N>1 or --no-pmc)"
     if world == 1 and not args.no_pmc:  # before this process touches the GPU
         traffic, traffic_detail = pmc_traffic(args)
-    local = local % max(1, torch.cuda.device_count())  # > 1 rank per GPU only in a gloo rehearsal
+    ndev = torch.cuda.device_count()
+    if world > 1 and args.dist_backend == "nccl" and world > ndev:
+        sys.exit(f"bench.py: WORLD_SIZE={world} ranks but {ndev} visible GPU(s): RCCL needs one GPU per rank "
+                 f"(use --dist-backend gloo to rehearse several ranks on one GPU)")
+    local = local % max(1, ndev)  # > 1 rank per GPU only in a gloo rehearsal
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:

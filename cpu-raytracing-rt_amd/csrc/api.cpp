@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -59,6 +60,11 @@ struct rt_scene {
     // the path kernel reads the scene record and the frame constants by pointer
     DevScene* d_scene = nullptr;
     KParams* d_params = nullptr;
+    // Completion of the last launch that used the workspace above (queue, ring,
+    // partials, spill, d_params).  Each workspace-using launch first makes its
+    // stream wait on it, then re-records it, so calls issued on different
+    // streams never overlap on the shared workspace.
+    hipEvent_t ws_done = nullptr;
 };
 
 namespace {
@@ -108,9 +114,46 @@ void free_scene(rt_scene* s) {
     if (s->d_stats) (void)hipFree(s->d_stats);
     if (s->d_scene) (void)hipFree(s->d_scene);
     if (s->d_params) (void)hipFree(s->d_params);
+    if (s->ws_done) (void)hipEventDestroy(s->ws_done);
     (void)hipSetDevice(cur);
     delete s;
 }
+
+struct SceneDeleter {
+    void operator()(rt_scene* s) const { free_scene(s); }
+};
+
+// Makes the scene's device current for one entry point and restores the
+// caller's current device on every return path.
+struct DeviceGuard {
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    explicit DeviceGuard(int dev) {
+        err = hipGetDevice(&prev);
+        if (err == hipSuccess && prev != dev) err = hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+#define DEVICE_GUARD(s)                                                                       \
+    DeviceGuard guard_((s)->device);                                                          \
+    if (guard_.err != hipSuccess)                                                             \
+        return set_error(RT_ERR_DEVICE, std::string("hipSetDevice: ") + hipGetErrorString(guard_.err))
+
+struct EventPair {  // hipEvent_t pair destroyed on every return path
+    hipEvent_t a = nullptr, b = nullptr;
+    ~EventPair() {
+        if (a) (void)hipEventDestroy(a);
+        if (b) (void)hipEventDestroy(b);
+    }
+};
+
+// Stream ordering of the shared workspace: wait for the previous user, launch,
+// then record (ws_begin / ws_end bracket every workspace-using launch).
+hipError_t ws_begin(rt_scene* s, hipStream_t st) { return hipStreamWaitEvent(st, s->ws_done, 0); }
+hipError_t ws_end(rt_scene* s, hipStream_t st) { return hipEventRecord(s->ws_done, st); }
 
 int check_params(const rt_render_params* p) {
     if (!p) return set_error(RT_ERR_INVALID, "params is NULL");
@@ -169,10 +212,17 @@ KParams make_kparams(const rt_render_params* p, uint32_t rank, uint32_t world) {
 
 uint32_t slots_per_rank(const KParams& k) { return k.n_slots; }
 
+// Before a workspace buffer is regrown: the last launch that used it is done.
+int ws_idle(rt_scene* s) {
+    HIP_TRY(hipEventSynchronize(s->ws_done));
+    return RT_OK;
+}
+
 int ensure_part(rt_scene* s, const KParams& k) {
     if (k.chunks == 1) return RT_OK;
     const size_t need = (size_t)k.n_slots * k.chunks * 256 * 3;
     if (need <= s->part_entries) return RT_OK;
+    if (int rc = ws_idle(s)) return rc;
     if (s->part) (void)hipFree(s->part);
     s->part = nullptr; s->part_entries = 0;
     HIP_TRY(hipMalloc(&s->part, need * sizeof(double)));
@@ -187,6 +237,7 @@ int ensure_spill(rt_scene* s, uint64_t lanes) {
     if (depth <= (uint32_t)kMaxBvhDepthShort) return RT_OK;
     size_t need = (size_t)(depth - kMaxBvhDepthShort) * lanes;
     if (need <= s->spill_entries) return RT_OK;
+    if (int rc = ws_idle(s)) return rc;
     if (s->spill_n) (void)hipFree(s->spill_n);
     if (s->spill_t) (void)hipFree(s->spill_t);
     s->spill_n = nullptr; s->spill_t = nullptr; s->spill_entries = 0;
@@ -236,6 +287,7 @@ int prepare_path(rt_scene* s, const KParams& k, bool stats, bool hits, PathWork&
     if (!s->queue) HIP_TRY(hipMalloc(&s->queue, kQueueWords * sizeof(uint32_t)));
     const size_t ring_need = (size_t)W.grid * kRingRows * 64 * 3;
     if (ring_need > s->ring_entries) {
+        if (int rc2 = ws_idle(s)) return rc2;
         if (s->ring) (void)hipFree(s->ring);
         s->ring = nullptr; s->ring_entries = 0;
         HIP_TRY(hipMalloc(&s->ring, ring_need * sizeof(double)));
@@ -287,8 +339,10 @@ int rt_scene_create(const rt_scene_desc* desc, rt_scene** out) {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
         return set_error(RT_ERR_DEVICE, "no HIP device visible (the hot path has no CPU fallback)");
-    rt_scene* s = new rt_scene();
+    std::unique_ptr<rt_scene, SceneDeleter> owner(new rt_scene());  // frees everything on an error return
+    rt_scene* s = owner.get();
     HIP_TRY(hipGetDevice(&s->device));
+    HIP_TRY(hipEventCreateWithFlags(&s->ws_done, hipEventDisableTiming));
     auto t0 = std::chrono::steady_clock::now();
     int rc = RT_OK;
     DevScene& d = s->dev;
@@ -297,10 +351,8 @@ int rt_scene_create(const rt_scene_desc* desc, rt_scene** out) {
         (rc = upload(s, hs.plane_gid, &d.plane_gid)) || (rc = upload(s, hs.mats, &d.mats)) ||
         (rc = upload_bvh(s, hs.bvh[0], d.boxes)) || (rc = upload_bvh(s, hs.bvh[1], d.ells)) ||
         (rc = upload_bvh(s, hs.bvh[2], d.tris)) || (rc = upload_bvh(s, hs.bvh[3], d.lboxes)) ||
-        (rc = upload_bvh(s, hs.bvh[4], d.lells)) || (rc = upload_bvh(s, hs.bvh[5], d.ltris))) {
-        free_scene(s);
+        (rc = upload_bvh(s, hs.bvh[4], d.lells)) || (rc = upload_bvh(s, hs.bvh[5], d.ltris)))
         return rc;
-    }
     {  // world normals of plane sides and box faces: rotated(Hit, rot) of render.hip materialise
         std::vector<double> pn(hs.planes.size() * 6), bn(hs.bvh[0].shapes.size() * 24, 0.0);
         for (size_t i = 0; i < hs.planes.size(); ++i) {
@@ -319,10 +371,7 @@ int rt_scene_create(const rt_scene_desc* desc, rt_scene** out) {
                 store3(&bn[i * 24 + a * 3], normalize(rotate(q, n)));
             }
         }
-        if ((rc = upload(s, pn, &d.plane_nrm)) || (rc = upload(s, bn, &d.box_nrm))) {
-            free_scene(s);
-            return rc;
-        }
+        if ((rc = upload(s, pn, &d.plane_nrm)) || (rc = upload(s, bn, &d.box_nrm))) return rc;
     }
     d.n_lights = d.lboxes.n_prims + d.lells.n_prims + d.ltris.n_prims;
     // UINT64_MAX - (2^64 - n) % n (oracle.c usize_zone); unused without lights
@@ -348,7 +397,7 @@ int rt_scene_create(const rt_scene_desc* desc, rt_scene** out) {
     s->info.n_light_triangles = d.ltris.n_prims;
     s->info.build_ms = hs.build_ms;
     s->info.upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    *out = s;
+    *out = owner.release();
     return RT_OK;
 }
 
@@ -382,17 +431,21 @@ int rt_render_tiles_async(rt_scene* s, const rt_render_params* p, uint32_t rank,
     if (rc) return rc;
     if (!s || !d_tile_rgb) return set_error(RT_ERR_INVALID, "scene/output is NULL");
     if (world == 0 || rank >= world) return set_error(RT_ERR_INVALID, "rank must be < world");
+    DEVICE_GUARD(s);
     KParams k = make_kparams(p, rank, world);
     const bool want_stats = (p->flags & RT_FLAG_STATS) != 0;
     PathWork W;
     if ((rc = prepare_path(s, k, want_stats, false, W))) return rc;
-    HIP_TRY(launch_path(s->dev, k, W, d_tile_rgb, nullptr, want_stats ? s->d_stats : nullptr, (hipStream_t)stream));
+    const hipStream_t st = (hipStream_t)stream;
+    HIP_TRY(ws_begin(s, st));
+    HIP_TRY(launch_path(s->dev, k, W, d_tile_rgb, nullptr, want_stats ? s->d_stats : nullptr, st));
+    HIP_TRY(ws_end(s, st));
     return RT_OK;
 }
 
 int rt_read_stats(rt_scene* s, rt_stats* out, int reset) {
     if (!s || !out) return set_error(RT_ERR_INVALID, "scene/out is NULL");
-    HIP_TRY(hipSetDevice(s->device));
+    DEVICE_GUARD(s);
     HIP_TRY(hipDeviceSynchronize());
     std::memset(out, 0, sizeof(*out));
     int rc = copy_stats(s, out);
@@ -403,7 +456,7 @@ int rt_read_stats(rt_scene* s, rt_stats* out, int reset) {
 
 int rt_read_raw_stats(rt_scene* s, uint64_t* out, uint32_t n) {
     if (!s || !out || n > (uint32_t)kStatsWords) return set_error(RT_ERR_INVALID, "scene/out NULL or n > 48");
-    HIP_TRY(hipSetDevice(s->device));
+    DEVICE_GUARD(s);
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(out, s->d_stats, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return RT_OK;
@@ -443,7 +496,7 @@ int rt_render(rt_scene* s, const rt_render_params* p, double* out_mean_rgb, int3
     int rc = check_params(p);
     if (rc) return rc;
     if (!s || !out_mean_rgb) return set_error(RT_ERR_INVALID, "scene/output is NULL");
-    HIP_TRY(hipSetDevice(s->device));
+    DEVICE_GUARD(s);
     KParams k = make_kparams(p, 0, 1);
     const uint32_t slots = slots_per_rank(k);
     const uint64_t npx = (uint64_t)p->width * p->height;
@@ -458,23 +511,20 @@ int rt_render(rt_scene* s, const rt_render_params* p, double* out_mean_rgb, int3
     const uint64_t nhits = npx * p->spp * p->ray_depth;
     if (want_hits) HIP_TRY(hits.alloc(nhits));
     if (want_stats) HIP_TRY(hipMemset(s->d_stats, 0, kStatsWords * sizeof(unsigned long long)));
-    hipEvent_t e0, e1;
-    HIP_TRY(hipEventCreate(&e0));
-    HIP_TRY(hipEventCreate(&e1));
-    HIP_TRY(hipEventRecord(e0, 0));
+    EventPair ev;
+    HIP_TRY(hipEventCreate(&ev.a));
+    HIP_TRY(hipEventCreate(&ev.b));
+    HIP_TRY(ws_begin(s, 0));
+    HIP_TRY(hipEventRecord(ev.a, 0));
     hipError_t le = launch_path(s->dev, k, W, tiles.p, want_hits ? hits.p : nullptr,
                                 want_stats ? s->d_stats : nullptr, 0);
-    HIP_TRY(hipEventRecord(e1, 0));
-    if (le != hipSuccess) {
-        (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
-        return set_error(RT_ERR_DEVICE, std::string("path kernel launch: ") + hipGetErrorString(le));
-    }
+    HIP_TRY(hipEventRecord(ev.b, 0));
+    if (le != hipSuccess) return set_error(RT_ERR_DEVICE, std::string("path kernel launch: ") + hipGetErrorString(le));
+    HIP_TRY(ws_end(s, 0));
     HIP_TRY(launch_unpack(tiles.p, img.p, p->width, p->height, k.tiles_x, 1, slots, 0));
     HIP_TRY(hipDeviceSynchronize());
     float ms = 0.f;
-    (void)hipEventElapsedTime(&ms, e0, e1);
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
+    (void)hipEventElapsedTime(&ms, ev.a, ev.b);
     HIP_TRY(hipMemcpy(out_mean_rgb, img.p, npx * 3 * sizeof(double), hipMemcpyDeviceToHost));
     if (want_hits) HIP_TRY(hipMemcpy(opt_hit_ids, hits.p, nhits * sizeof(int32_t), hipMemcpyDeviceToHost));
     if (opt_stats) {
@@ -489,7 +539,7 @@ int rt_render(rt_scene* s, const rt_render_params* p, double* out_mean_rgb, int3
 int rt_intersect_rays(rt_scene* s, const double* rays, uint32_t n, rt_hit* out) {
     if (!s || (!rays && n) || (!out && n)) return set_error(RT_ERR_INVALID, "bad arguments");
     if (n == 0) return RT_OK;
-    HIP_TRY(hipSetDevice(s->device));
+    DEVICE_GUARD(s);
     int rc = ensure_spill(s, ((uint64_t)n + 255) / 256 * 256);
     if (rc) return rc;
     DevBuf<double> r;
@@ -497,7 +547,9 @@ int rt_intersect_rays(rt_scene* s, const double* rays, uint32_t n, rt_hit* out) 
     HIP_TRY(r.alloc((size_t)n * 6));
     HIP_TRY(h.alloc(n));
     HIP_TRY(hipMemcpy(r.p, rays, (size_t)n * 6 * sizeof(double), hipMemcpyHostToDevice));
+    HIP_TRY(ws_begin(s, 0));
     HIP_TRY(launch_intersect(s->dev, r.p, n, h.p, s->spill_n, s->spill_t, 0));
+    HIP_TRY(ws_end(s, 0));
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(out, h.p, (size_t)n * sizeof(rt_hit), hipMemcpyDeviceToHost));
     return RT_OK;
@@ -508,12 +560,14 @@ int rt_intersect_rays_async(rt_scene* s, const double* d_rays, uint32_t n, rt_hi
     if (!s || (!d_rays && n) || (!d_out && n)) return set_error(RT_ERR_INVALID, "bad arguments");
     if (method != RT_TRACE_PER_RAY && method != RT_TRACE_PERSISTENT) return set_error(RT_ERR_INVALID, "bad method");
     if (n == 0) return RT_OK;
-    HIP_TRY(hipSetDevice(s->device));
+    DEVICE_GUARD(s);
     const hipStream_t st = (hipStream_t)hip_stream;
     if (method == RT_TRACE_PER_RAY) {
         int rc = ensure_spill(s, ((uint64_t)n + 255) / 256 * 256);
         if (rc) return rc;
+        HIP_TRY(ws_begin(s, st));
         HIP_TRY(launch_intersect(s->dev, d_rays, n, d_out, s->spill_n, s->spill_t, st));
+        HIP_TRY(ws_end(s, st));
         return RT_OK;
     }
     uint32_t grid = 0;
@@ -523,14 +577,16 @@ int rt_intersect_rays_async(rt_scene* s, const double* d_rays, uint32_t n, rt_hi
     int rc = ensure_spill(s, (uint64_t)grid * 64);
     if (rc) return rc;
     if (!s->queue) HIP_TRY(hipMalloc(&s->queue, kQueueWords * sizeof(uint32_t)));
+    HIP_TRY(ws_begin(s, st));
     HIP_TRY(launch_trace(s->dev, d_rays, n, d_out, s->queue, s->spill_n, s->spill_t, grid, st));
+    HIP_TRY(ws_end(s, st));
     return RT_OK;
 }
 
 static int light_query(rt_scene* s, const double* rays, uint32_t n, int mode, double* out, uint32_t* cnt) {
     if (!s || (!rays && n) || (!out && n)) return set_error(RT_ERR_INVALID, "bad arguments");
     if (n == 0) return RT_OK;
-    HIP_TRY(hipSetDevice(s->device));
+    DEVICE_GUARD(s);
     int rc = ensure_spill(s, ((uint64_t)n + 255) / 256 * 256);
     if (rc) return rc;
     DevBuf<double> r, o;
@@ -539,7 +595,9 @@ static int light_query(rt_scene* s, const double* rays, uint32_t n, int mode, do
     HIP_TRY(o.alloc(n));
     if (cnt) HIP_TRY(c.alloc(n));
     HIP_TRY(hipMemcpy(r.p, rays, (size_t)n * 6 * sizeof(double), hipMemcpyHostToDevice));
+    HIP_TRY(ws_begin(s, 0));
     HIP_TRY(launch_light(s->dev, r.p, n, mode, o.p, cnt ? c.p : nullptr, s->spill_n, s->spill_t, 0));
+    HIP_TRY(ws_end(s, 0));
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(out, o.p, (size_t)n * sizeof(double), hipMemcpyDeviceToHost));
     if (cnt) HIP_TRY(hipMemcpy(cnt, c.p, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost));

@@ -19,6 +19,14 @@
  *  - Numerics: f64 everywhere, like the reference (src/types.rs:5).
  *  - Threading: one host thread per handle (a handle is not re-entrant), as
  *    the reference calls its pixel loop once from the main thread.
+ *  - Devices: a scene lives on the device that was current at rt_scene_create.
+ *    Every call taking a scene switches to that device for its duration and
+ *    restores the caller's current device before returning.
+ *  - Streams: launches that use a scene's shared workspace (queue, sample ring,
+ *    chunk partials, stack spill) are ordered by the library: each waits for
+ *    the previous one on that scene through an event, whatever stream either
+ *    was issued on.  Calls on different streams therefore never overlap on one
+ *    scene (they serialise); use one scene per stream for concurrency.
  */
 #ifndef RT_API_H
 #define RT_API_H
@@ -189,8 +197,8 @@ int rt_render(rt_scene* scene, const rt_render_params* params,
    asynchronously on `hip_stream` (NULL = default stream). */
 #define RT_TILE 16
 int rt_tiles_per_rank(const rt_render_params* params, uint32_t world, uint32_t* n_tiles_padded);
-/* The scene's per-call workspace (stack spill, chunk partials) is shared: one
-   scene renders on one stream at a time. */
+/* The scene's per-call workspace (stack spill, chunk partials) is shared;
+   successive calls are ordered on it across streams (Conventions: Streams). */
 int rt_render_tiles_async(rt_scene* scene, const rt_render_params* params,
                           uint32_t rank, uint32_t world,
                           double* d_tile_rgb, void* hip_stream);
@@ -234,8 +242,8 @@ int rt_intersect_rays(rt_scene* scene, const double* rays, uint32_t n, rt_hit* o
 /* The same query on device-resident buffers, stream-ordered (no host copies):
    d_rays [n][6] f64 and d_out [n] rt_hit in HBM.  method 0 runs one thread per
    ray; method 1 the persistent traversal (waves refill finished lanes from a
-   queue).  Both give identical hits.  Uses the scene's workspace, so one
-   launch per scene at a time (like rt_render_tiles_async). */
+   queue).  Both give identical hits.  Uses the scene's workspace, ordered
+   after the scene's previous launch (Conventions: Streams). */
 #define RT_TRACE_PER_RAY    0
 #define RT_TRACE_PERSISTENT 1
 int rt_intersect_rays_async(rt_scene* scene, const double* d_rays, uint32_t n, rt_hit* d_out, int method,

@@ -228,6 +228,30 @@ def test_tile_partition_matches_single(cornell, rt):
     assert np.array_equal(img.cpu().numpy(), ref)
 
 
+def test_workspace_ordered_across_streams(cornell, rt):
+    """Calls on one scene issued on different streams share its workspace
+    (queue, ring, partials): the library orders them with an event, so
+    back-to-back launches on two streams with no host sync still give the
+    single-stream result, rank after rank (rt_api.h Conventions: Streams)."""
+    torch = pytest.importorskip("torch")
+    desc, params, g, o = cornell
+    p = params.replace(width=96, height=64, spp=8)
+    ref, _, _ = g.generate_image(p)
+    world = 4
+    per = g.tiles_per_rank(p, world)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    gathered = torch.zeros((world, per, 256, 3), dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    for r in range(world):
+        g.render_tiles_async(p, r, world, gathered[r].data_ptr(), streams[r % 2].cuda_stream)
+    torch.cuda.synchronize()
+    img = torch.zeros((p.height, p.width, 3), dtype=torch.float64, device="cuda")
+    rt.unpack_tiles_async(p, world, gathered.data_ptr(), img.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(img.cpu().numpy(), ref)
+    assert torch.cuda.current_device() == 0  # the device guard restores the caller's device
+
+
 def test_no_lights_scene(rt, orc):
     text = """DIMENSIONS 20 16
 SAMPLES 3
