@@ -14,9 +14,10 @@ per-frame segment count is counted on the device in an untimed pass.
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
-Rank 0 prints ONE JSON line.  Extras: "roofline" (canonical algorithmic bytes
-of the path kernel, DESIGN.md §4, over its HIP-event-timed launch duration)
-and "cpu_baseline" (the oracle, the C restatement of the reference, timed on
+Rank 0 prints ONE JSON line.  Extras: "roofline" (the path kernel's f64 VALU
+issue roofline: PMC instruction mix of its launch over the chip's issue limit,
+timed by HIP events; plus its measured HBM rate and the SURVEY §8d algorithmic
+byte rate) and "cpu_baseline" (the oracle, the C restatement of the reference, timed on
 a bounded row window of the same frame on the host cores; rank 0, N=1 only).
 """
 import argparse
@@ -79,45 +80,114 @@ def algo_bytes(st):
 
 PATH_KERNEL = "path_kernel<false, false,"  # the timed instance (any waves/SIMD budget)
 
+# VALU issue roofline.  The path kernel is f64 VALU-issue bound,
+# not HBM- or MFMA-bound.  Issue cost of one wave64 VALU instruction on a gfx950
+# SIMD, in shader cycles: 2 for 32-bit ops (MI355X_MICROARCH.md "Wave
+# scheduling": 32 lanes/cycle x 2), and from tools/valu_rates.hip with every
+# SIMD loaded (profiles/r02/valu_rates.log, 8 waves/SIMD): v_fma/mul/add_f64
+# 4.2, v_rcp_f64 16.2, v_mad_u64_u32 4.5.  Instructions outside the counted
+# classes (compares, cndmask, moves, f32, int32) are priced at the 2-cycle
+# floor, although v_cmp_*_f64 and v_cndmask_b32 measure ~4: the busy fraction
+# below is therefore a LOWER bound.
+SIMDS = 256 * 4
+MAX_CLOCK_HZ = 2.4e9
+VALU_CYCLES = {"f64": 4.0, "trans_f64": 16.0, "int64": 4.0, "other": 2.0}
+PMC_PASSES = (
+    # (counters, one pass each: <= 8 SQ, <= 4 TCC (FETCH_SIZE uses 3, WRITE_SIZE 2), <= 2 GRBM)
+    ("FETCH_SIZE", "SQ_THREAD_CYCLES_VALU", "SQ_ACTIVE_INST_VALU"),
+    ("WRITE_SIZE",),
+    ("SQ_INSTS_VALU", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64",
+     "SQ_INSTS_VALU_TRANS_F64", "SQ_INSTS_VALU_INT64", "GRBM_GUI_ACTIVE"),
+)
 
-def pmc_traffic(args):
-    """HBM bytes per launch of the timed path kernel, from two child rocprofv3
-    --pmc passes (FETCH_SIZE, then WRITE_SIZE: they do not fit one TCC pass) of
-    this same workload, run BEFORE this process initialises the GPU.  Correction
-    per MI355X_MICROARCH.md "HBM": FETCH_SIZE is in KiB and reports half the
-    bytes of 16-B/lane loads on gfx950 (the node/triangle loads are dwordx4),
-    so fetch bytes = 2 * 1024 * FETCH_SIZE; WRITE_SIZE is taken as reported."""
+
+def pmc_counters(args, world):
+    """Counters of the timed path kernel's launch, from child rocprofv3 --pmc
+    passes of this same workload (rank 0's tile share of a world-`world`
+    partition), run BEFORE this process initialises the GPU.  Returns
+    ({counter: value}, dispatch_ns) or (None, reason)."""
     import csv
     import shutil
     import subprocess
     import tempfile
     if shutil.which("rocprofv3") is None:
         return None, "rocprofv3 not found"
-    vals = {}
+    vals, ns = {}, None
     with tempfile.TemporaryDirectory(prefix="rt_pmc_") as td:
-        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
-            d = os.path.join(td, counter)
-            cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "run", "--",
+        for i, counters in enumerate(PMC_PASSES):
+            d = os.path.join(td, f"p{i}")
+            cmd = ["rocprofv3", "--pmc", *counters, "--output-format", "csv", "-d", d, "-o", "run", "--",
                    sys.executable, os.path.abspath(__file__), "--workload", args.workload, "--steps", "1",
-                   "--warmup", "0", "--no-cpu-baseline", "--no-pmc"] + (["--spp", str(args.spp)] if args.spp else [])
+                   "--warmup", "0", "--no-cpu-baseline", "--no-pmc", "--as-rank0-of", str(world)]
+            cmd += ["--spp", str(args.spp)] if args.spp else []
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
             if r.returncode != 0:
-                return None, f"rocprofv3 --pmc {counter} failed rc={r.returncode}: {r.stderr[-300:]}"
+                return None, f"rocprofv3 --pmc {' '.join(counters)} failed rc={r.returncode}: {r.stderr[-300:]}"
             rows = []
             for root, _, files in os.walk(d):
                 for f in files:
                     if f.endswith("counter_collection.csv"):
-                        rows += [x for x in csv.DictReader(open(os.path.join(root, f)))
-                                 if PATH_KERNEL in x["Kernel_Name"] and x["Counter_Name"] == counter]
+                        rows += [x for x in csv.DictReader(open(os.path.join(root, f))) if PATH_KERNEL in x["Kernel_Name"]]
             if not rows:
-                return None, f"no {counter} rows for {PATH_KERNEL}"
-            vals[counter] = float(rows[-1]["Counter_Value"])
-    fetch = 2.0 * 1024.0 * vals["FETCH_SIZE"]
-    write = 1024.0 * vals["WRITE_SIZE"]
-    return fetch + write, {"FETCH_SIZE_KiB": vals["FETCH_SIZE"], "WRITE_SIZE_KiB": vals["WRITE_SIZE"],
+                return None, f"no rows for {PATH_KERNEL} in the pass {counters}"
+            last = max(int(x["Dispatch_Id"]) for x in rows)  # the timed launch (the first is the counting pass)
+            for x in rows:
+                if int(x["Dispatch_Id"]) == last:
+                    vals[x["Counter_Name"]] = vals.get(x["Counter_Name"], 0.0) + float(x["Counter_Value"])
+                    ns = int(x["End_Timestamp"]) - int(x["Start_Timestamp"])
+    missing = [c for p in PMC_PASSES for c in p if c not in vals]
+    if missing:
+        return None, f"counters missing: {missing}"
+    return vals, ns
+
+
+def hbm_traffic(pmc):
+    """HBM bytes per launch.  Correction per MI355X_MICROARCH.md "HBM": FETCH_SIZE
+    is in KiB and reports half the bytes of 16-B/lane loads on gfx950 (the
+    node/triangle loads are dwordx4), so fetch = 2 * 1024 * FETCH_SIZE;
+    WRITE_SIZE is taken as reported (KiB)."""
+    fetch = 2.0 * 1024.0 * pmc["FETCH_SIZE"]
+    write = 1024.0 * pmc["WRITE_SIZE"]
+    return fetch + write, {"FETCH_SIZE_KiB": pmc["FETCH_SIZE"], "WRITE_SIZE_KiB": pmc["WRITE_SIZE"],
                            "fetch_bytes": fetch, "write_bytes": write,
                            "correction": "fetch = 2 x 1024 x FETCH_SIZE (gfx950 16-B/lane loads); "
                                          "write = 1024 x WRITE_SIZE", "kernel": PATH_KERNEL}
+
+
+def valu_roofline(pmc, pmc_ns, kern_s):
+    """VALU issue roofline of the path kernel: wave-instructions per second over
+    the instruction-mix-weighted issue limit of the chip's 1024 SIMDs."""
+    n = pmc["SQ_INSTS_VALU"]
+    f64 = pmc["SQ_INSTS_VALU_FMA_F64"] + pmc["SQ_INSTS_VALU_MUL_F64"] + pmc["SQ_INSTS_VALU_ADD_F64"]
+    trans, i64 = pmc["SQ_INSTS_VALU_TRANS_F64"], pmc["SQ_INSTS_VALU_INT64"]
+    other = max(0.0, n - f64 - trans - i64)
+    busy = (VALU_CYCLES["f64"] * f64 + VALU_CYCLES["trans_f64"] * trans + VALU_CYCLES["int64"] * i64 +
+            VALU_CYCLES["other"] * other)  # SIMD issue cycles the launch needs
+    # shader clock of the profiled launch: GRBM_GUI_ACTIVE is summed over the 8 XCDs
+    clk = pmc["GRBM_GUI_ACTIVE"] / 8.0 / (pmc_ns * 1e-9) if pmc_ns else 0.0
+    clk_used = clk if 1.0e9 <= clk <= MAX_CLOCK_HZ else MAX_CLOCK_HZ
+    frac = busy / (SIMDS * clk_used * kern_s)
+    achieved = n / kern_s / 1e9
+    lanes = pmc["SQ_THREAD_CYCLES_VALU"] / pmc["SQ_ACTIVE_INST_VALU"]
+    return {
+        "bound": "valu",
+        "achieved": achieved,
+        "peak": achieved / frac,
+        "unit": "G wave64 VALU instr/s",
+        "frac": frac,
+        "valu_detail": {
+            "instr_per_launch": n, "f64_fma_mul_add": f64, "f64_trans": trans, "int64": i64, "other": other,
+            "issue_cycles_per_instr": VALU_CYCLES, "busy_simd_cycles": busy,
+            "clock_GHz": clk_used / 1e9, "clock_measured_GHz": clk / 1e9,
+            "active_lanes_per_instr": lanes, "lane_util": lanes / 64.0,
+            "useful_lane_frac": frac * lanes / 64.0,
+            "hw_active_frac": 4.0 * pmc["SQ_ACTIVE_INST_VALU"] / (SIMDS * clk_used * kern_s),
+            "peak_note": "peak = the same instruction mix issued back to back on all 1024 SIMDs at the measured "
+                         "clock; frac = busy SIMD cycles / available (a lower bound: uncounted classes at the "
+                         "2-cycle floor); useful_lane_frac = frac x active lanes / 64 (divergence); "
+                         "hw_active_frac = SQ_ACTIVE_INST_VALU quad-cycles x 4 / available cycles",
+        },
+    }
 
 
 def cpu_baseline(desc, params, target_s):
@@ -168,7 +238,8 @@ def main():
     ap.add_argument("--spp", type=int, default=None, help="override spp (not the headline config)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc child passes (traffic=null)")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc child passes (roofline=null)")
+    ap.add_argument("--as-rank0-of", type=int, default=0, help=argparse.SUPPRESS)  # PMC child: rank 0's share
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (RCCL over xGMI, the product path); gloo gathers host copies and lets several "
                          "ranks share one GPU (a rehearsal of the N>1 path on a one-GPU box)")
@@ -177,9 +248,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    traffic, traffic_detail = None, "not collected (N>1 or --no-pmc)"
-    if world == 1 and not args.no_pmc:  # before this process touches the GPU
-        traffic, traffic_detail = pmc_traffic(args)
+    pmc, pmc_ns = None, "not collected (--no-pmc)"
+    if rank == 0 and not args.no_pmc and not args.as_rank0_of:  # before this process touches the GPU
+        pmc, pmc_ns = pmc_counters(args, world)
     ndev = torch.cuda.device_count()
     if world > 1 and args.dist_backend == "nccl" and world > ndev:
         sys.exit(f"bench.py: WORLD_SIZE={world} ranks but {ndev} visible GPU(s): RCCL needs one GPU per rank "
@@ -204,7 +275,9 @@ def main():
     scene = rt.Scene(desc)
     build_s = time.perf_counter() - t0
 
-    per = scene.tiles_per_rank(params, world)
+    # a PMC child renders rank 0's tile share of the parent's partition, alone
+    part = args.as_rank0_of or world
+    per = scene.tiles_per_rank(params, part)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
     tiles = torch.empty((per, 256, 3), dtype=torch.float64, device=dev)
@@ -214,7 +287,7 @@ def main():
 
     # untimed counting pass: this rank's work of one frame
     scene.read_stats(reset=True)
-    scene.render_tiles_async(params, rank, world, tiles.data_ptr(), sptr, stats=True)
+    scene.render_tiles_async(params, rank, part, tiles.data_ptr(), sptr, stats=True)
     st = scene.read_stats(reset=True)
     seg = torch.tensor([st["segments"], st["paths"]], dtype=torch.float64, device=dev)
     if world > 1:
@@ -227,10 +300,12 @@ def main():
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-        scene.render_tiles_async(params, rank, world, tiles.data_ptr(), sptr)
+        scene.render_tiles_async(params, rank, part, tiles.data_ptr(), sptr)
         if timed:
             e1.record(stream)
             ev.append((e0, e1))
+        if part != world:  # PMC child: only the path kernel is of interest
+            return
         if args.dist_backend == "nccl" or world == 1:
             src = rt.gather_tiles(tiles, gathered, rank, world)
         else:  # gloo: the same single gather on host copies
@@ -260,9 +335,35 @@ def main():
     elapsed = float(tt.item())
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
 
+    if rank == 0 and part != world:  # PMC child: nothing to report
+        return
     if rank == 0:
         value = frame_segments * args.steps / elapsed / 1e6
-        achieved = algo_bytes(st) / (kern_ms * 1e-3) / 1e9
+        kern_s = kern_ms * 1e-3
+        algo = algo_bytes(st)
+        if pmc is None:
+            roofline = {"bound": "valu", "achieved": None, "peak": None, "unit": "G wave64 VALU instr/s",
+                        "frac": None, "traffic": None, "note": f"PMC passes unavailable: {pmc_ns}"}
+        else:
+            roofline = valu_roofline(pmc, pmc_ns, kern_s)
+            traffic, detail = hbm_traffic(pmc)
+            roofline["traffic"] = traffic
+            roofline["hbm"] = {"achieved_GBps": traffic / kern_s / 1e9, "peak_GBps": HBM_PEAK_GBS,
+                               "frac": traffic / kern_s / 1e9 / HBM_PEAK_GBS, "detail": detail}
+        roofline.update({
+            "kernel": "rt::path_kernel<false,false,W,RES> (W = waves/SIMD budget, RES = resumable traversal; "
+                      "both chosen per scene)",
+            "kernel_ms": kern_ms,
+            "pmc_kernel_ms": (pmc_ns * 1e-6) if isinstance(pmc_ns, int) else None,
+            # the SURVEY §8d canonical bytes: what the reference's data layout would move per
+            # launch.  The kernel serves them from L1/L2/scalar cache/MALL, so their rate is a
+            # cache-level throughput, not an HBM one, and is not used as `frac`
+            "algorithmic": {"bytes_per_launch": algo, "GBps": algo / kern_s / 1e9,
+                            "model": "32*aabb_tests + 72*tri_tests + 80*shape_tests + 100*shaded_hits "
+                                     "(rank 0 tiles)"},
+            "note": "bound = f64 VALU issue: frac = VALU busy SIMD-cycles / available (valu_detail); the "
+                    "measured HBM rate is roofline.hbm (traffic = PMC HBM bytes per launch)",
+        })
         out = {
             "metric": "Msamples/s (rays traced x bounces) at 1920x1080, 256 spp; fraction of HBM roofline",
             "value": value,
@@ -287,26 +388,7 @@ def main():
                 "epilogue": "device unpack + ACES + gamma + PPM bytes (rt_unpack_tiles_bytes_async)",
                 "seed": params.seed,
             },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic,
-                "traffic_detail": traffic_detail,
-                "kernel": "rt::path_kernel<false,false,W,RES> (W = waves/SIMD budget, RES = resumable traversal; both chosen per scene)",
-                "kernel_ms": kern_ms,
-                "algorithmic_bytes_per_launch": algo_bytes(st),
-                "bytes_model": "32*aabb_tests + 72*tri_tests + 80*shape_tests + 100*shaded_hits (rank 0 tiles)",
-                # the SURVEY §8d bytes are what the reference's data layout would move; the
-                # kernel serves them from L1/L2/K$/MALL (C2's scene is < 4 KB), so `frac` can
-                # exceed 1.  The measured HBM side is `traffic` over the same launch:
-                "traffic_frac": (traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
-                "note": "frac = algorithmic (SURVEY 8d) bytes per launch / launch time / HBM peak; the bytes "
-                        "are cache-served, so frac > 1 is possible and the kernel's real bound is f64 VALU "
-                        "issue + divergence (DESIGN.md 4); traffic_frac = measured HBM bytes / time / peak",
-            },
+            "roofline": roofline,
             "paths_per_s": frame_paths * args.steps / elapsed,
             "scene_build_s": build_s,
         }

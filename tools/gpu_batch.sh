@@ -4,7 +4,7 @@
 # kernel dispatches).  Every GPU step has its own time limit and the chain stops
 # at the first failure.
 #   gpurun --timeout 1200 -- bash tools/gpu_batch.sh <tag> [steps...]
-# steps: tests c2 c3 prof2 prof3 pmc2 pmc3 occ2 (default: all)
+# steps: tests bench c2 c3 c5 prof2 prof3 pmc2 pmc3 occ2 mix2 eff2 ... (default: the list below)
 set -o pipefail
 cd "$(dirname "$0")/.." || exit 1
 export TMPDIR=/tmp
@@ -23,23 +23,24 @@ run() {  # run <name> <seconds> <cmd...>
 }
 for s in $STEPS; do
   case $s in
-    tests) run pytest_gpu 900 python3 -m pytest tests -m gpu -x -q || exit 1 ;;
+    tests) run pytest_gpu 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread || exit 1 ;;
+    bench) run bench_default 900 $B --gpus 1 --steps 20 --warmup 5 || exit 1 ;;
     c2)    run bench_c2 600 $B --workload C2 --steps 3 --warmup 1 || exit 1 ;;
     c3)    run bench_c3 600 $B --workload C3 --steps 3 --warmup 1 || exit 1 ;;
     c5)    run bench_c5 900 $B --workload C5 --steps 2 --warmup 1 || exit 1 ;;
     prof2) run prof_c2 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c2" -o run \
-             -- $B --workload C2 --steps 2 --warmup 1 --no-cpu-baseline || exit 1 ;;
+             -- $B --workload C2 --steps 2 --warmup 1 --no-cpu-baseline --no-pmc || exit 1 ;;
     prof3) run prof_c3 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c3" -o run \
-             -- $B --workload C3 --steps 2 --warmup 1 --no-cpu-baseline || exit 1 ;;
+             -- $B --workload C3 --steps 2 --warmup 1 --no-cpu-baseline --no-pmc || exit 1 ;;
     pmc2|pmc3)
       w=C${s#pmc}
       run fetch_$w 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch_$w" -o run \
-        -- $B --workload $w --steps 1 --warmup 0 --no-cpu-baseline || exit 1
+        -- $B --workload $w --steps 1 --warmup 0 --no-cpu-baseline --no-pmc || exit 1
       run write_$w 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write_$w" -o run \
-        -- $B --workload $w --steps 1 --warmup 0 --no-cpu-baseline || exit 1 ;;
+        -- $B --workload $w --steps 1 --warmup 0 --no-cpu-baseline --no-pmc || exit 1 ;;
     occ2)  run occ_C2 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
              --output-format csv -d "$OUT/occ_C2" -o run \
-             -- $B --workload C2 --steps 1 --warmup 0 --no-cpu-baseline || exit 1 ;;
+             -- $B --workload C2 --steps 1 --warmup 0 --no-cpu-baseline --no-pmc || exit 1 ;;
     ctrs)  run counters 300 rocprofv3 -L || exit 1 ;;
     mix2|mix3)  # SQ instruction mix + stall cycles of the path kernel (one SQ pass, 8 slots)
       w=C${s#mix}
