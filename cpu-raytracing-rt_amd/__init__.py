@@ -98,7 +98,8 @@ class rt_scene_info(C.Structure):
     _fields_ = [("n_planes", C.c_uint32), ("n_boxes", C.c_uint32), ("n_ellipsoids", C.c_uint32),
                 ("n_triangles", C.c_uint64), ("n_light_boxes", C.c_uint32), ("n_light_ellipsoids", C.c_uint32),
                 ("n_light_triangles", C.c_uint64), ("bvh_nodes", C.c_uint64 * 6), ("bvh_depth", C.c_uint32 * 6),
-                ("build_ms", C.c_double), ("upload_ms", C.c_double), ("device_bytes", C.c_uint64)]
+                ("build_ms", C.c_double), ("upload_ms", C.c_double), ("device_bytes", C.c_uint64),
+                ("shared_light_mask", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 # every symbol include/rt_api.h declares (checked by tests/test_abi.py)

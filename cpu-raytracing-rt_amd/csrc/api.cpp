@@ -309,6 +309,21 @@ int copy_stats(rt_scene* s, rt_stats* out) {
     return RT_OK;
 }
 
+// DevScene::slt_mask: the scene boxes (BVH order) that are the light boxes, in
+// order, when the light pdf can come from the closest-hit box tests (render.hip
+// boxes_slt): only box lights, both box BVHs single leaves (bvh.rs:77), and the
+// light copies (scene.rs:209-213) byte-identical to the selected scene records.
+uint32_t slt_mask(const HostScene& hs) {
+    const auto &B = hs.bvh[0], &L = hs.bvh[3];
+    if (L.shapes.empty() || !hs.bvh[4].shapes.empty() || !hs.bvh[5].tris.empty()) return 0;
+    if (B.depth != 1 || L.depth != 1 || B.shapes.size() > 32) return 0;
+    uint32_t mask = 0;
+    size_t j = 0;
+    for (size_t i = 0; i < B.shapes.size() && j < L.shapes.size(); ++i)
+        if (std::memcmp(&B.shapes[i], &L.shapes[j], sizeof(DevShape)) == 0) { mask |= 1u << i; ++j; }
+    return j == L.shapes.size() ? mask : 0;
+}
+
 template <class T>
 struct DevBuf {  // RAII device buffer for per-call scratch
     T* p = nullptr;
@@ -376,6 +391,7 @@ int rt_scene_create(const rt_scene_desc* desc, rt_scene** out) {
     d.n_lights = d.lboxes.n_prims + d.lells.n_prims + d.ltris.n_prims;
     // UINT64_MAX - (2^64 - n) % n (oracle.c usize_zone); unused without lights
     d.light_zone = d.n_lights ? UINT64_MAX - (0ull - (uint64_t)d.n_lights) % (uint64_t)d.n_lights : 0;
+    d.slt_mask = slt_mask(hs);
     d.max_depth = 0;
     const DevBvh* all[6] = {&d.boxes, &d.ells, &d.tris, &d.lboxes, &d.lells, &d.ltris};
     for (int k = 0; k < 6; ++k) {
@@ -395,6 +411,7 @@ int rt_scene_create(const rt_scene_desc* desc, rt_scene** out) {
     s->info.n_light_boxes = d.lboxes.n_prims;
     s->info.n_light_ellipsoids = d.lells.n_prims;
     s->info.n_light_triangles = d.ltris.n_prims;
+    s->info.shared_light_mask = d.slt_mask;
     s->info.build_ms = hs.build_ms;
     s->info.upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     *out = owner.release();

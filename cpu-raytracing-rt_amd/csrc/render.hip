@@ -485,13 +485,97 @@ RT_D Hit materialise(const DevScene& S, const Cand& c, V3 o, V3 d, Quat& rot, ui
     return h;
 }
 
+// One box of a single-leaf box BVH: box_coef on the model-space ray, exactly
+// as shape_closest<1> (closest hit) and leaf_all<1> (light pdf) compute it —
+// the fast and generic forms give the same bits.
+RT_D int box_test(const DevShape& s, V3 o, V3 d, const Rcp3& rc, bool rfast, Bpi& en, Bpi& ex) {
+    V3 mo, md;
+#ifndef RT_NO_FASTSHAPE
+    if (shape_fast(s, rfast, o, mo)) return box_coef<true>(load3(s.shape), mo, d, rc, en, ex);
+#endif
+    const bool same = model_ray(s, o, d, mo, md);
+    return box_coef(load3(s.shape), mo, md, same ? rc : make_rcp3(md), en, ex);
+}
+// The Light::pdf callback terms of one light box crossing (leaf_all<1>:
+// intersection_probability.rs:15-23, ray_sampler.rs:132-139,172-174)
+template <bool ST>
+RT_D void box_light_terms(const DevShape& s, int k, const Bpi& en, const Bpi& ex, V3 d, Cnt<ST>& C,
+                          double& impact) {
+    const double pb = s.aux[0];
+    const Quat q = load_quat(s.rot);
+    const bool qid = is_identity(q);
+    if (k == 2) {
+        const double dn = qid ? fabs(comp(d, en.dim)) : fabs(dot(d, normalize(rotate(q, bpi_normal(en)))));
+        impact += pb * (en.t * en.t / dn);
+        C.lhit();
+    }
+    if (k >= 1) {
+        const double dn = qid ? fabs(comp(d, ex.dim)) : fabs(dot(d, normalize(rotate(q, bpi_normal(ex)))));
+        impact += pb * (ex.t * ex.t / dn);
+        C.lhit();
+    }
+}
+
+// Shared light tests (DevScene::slt_mask): the box part of `intersect` for a
+// single-leaf box BVH, which also yields the Light::pdf sum of the previous
+// diffuse bounce for lanes whose pdf is pending (`pend`).  That bounce's light
+// query ray (pos + dir * eps, dir) IS this segment's ray, and every light is a
+// box whose record equals scene box i of the mask, so each light crossing comes
+// from the box_coef this query computes anyway.  Per lane, the steps and
+// counters are those of bvh_closest (bvh.rs:27-36) followed by intersect_lights
+// (intersections.rs:87-91 over lboxes; lells and ltris are empty), including
+// both root AABB tests: a light box is tested for the pdf exactly when the
+// light BVH's root is hit, whatever the scene BVH's root test said.
+template <bool ST>
+RT_D void boxes_slt(const DevScene& S, V3 o, V3 d, const Rcp3& rc, bool rfast, bool pend, Cnt<ST>& C, bool& valid,
+                    double& bt, uint32_t& bp, uint32_t& baux, double& impact) {
+    const DevBvh& B = S.boxes;
+    const DevBvh& L = S.lboxes;
+    valid = false;
+    double t0;
+    C.aabb();
+    const bool sroot = (B.fast && rfast) ? aabb_hit<true>(load3(B.root_min), load3(B.root_max), o, d, rc, t0)
+                                         : aabb_hit<false>(load3(B.root_min), load3(B.root_max), o, d, rc, t0);
+    bool lroot = false;
+    if (pend) {
+        C.lq();
+        C.aabb();
+        lroot = slab<2>(L.root_min, L.root_max, o, d, rc, L.fast && rfast, t0);
+    }
+    const uint32_t np = uni_u32(B.n_prims), mask = uni_u32(S.slt_mask);
+    const RT_CAS DevShape* shapes = uni(B.shapes);
+    double best = INFINITY;
+    for (uint32_t i = 0; i < np; ++i) {
+        const bool lt = ((mask >> i) & 1u) && lroot;
+        if (!(sroot || lt)) continue;
+        const DevShape sh = shapes[i];
+        Bpi en, ex;
+        const int k = box_test(sh, o, d, rc, rfast, en, ex);
+        if (sroot) {
+            C.shape();
+            if (k > 0) {
+                const double t = k == 2 ? en.t : ex.t;
+                if (!valid || t < best) {  // update_best_intersection (bvh.rs:213-222)
+                    valid = true; best = t; bp = i; baux = k == 2 ? bpi_aux(en, false) : bpi_aux(ex, true);
+                }
+            }
+        }
+        if (lt) {
+            C.shape();
+            box_light_terms<ST>(sh, k, en, ex, d, C, impact);
+        }
+    }
+    if (valid) bt = best;
+}
+
 // intersect(ray, &scene.primitives, +inf) (intersections.rs:42-62) in three
 // parts, so the path kernel can traverse the triangle BVH resumably:
 // shapes_closest (planes, boxes, ellipsoids: :45-55), take_tri (triangles
 // last, strict <: :55), intersect_tail (:56-61).
-template <bool ST, bool TF, class Stk>
+// SLT: the fused path kernel's form, with the shared light tests of boxes_slt.
+template <bool ST, bool TF, class Stk, bool SLT = false>
 RT_D void shapes_closest(const DevScene& S, V3 o, V3 d, const Rcp3& rc, bool rfast, Stk& stk, Cnt<ST>& C,
-                         Cand& best) {
+                         Cand& best, bool pend = false, double* impact = nullptr) {
     best.valid = false; best.t = 0.0; best.u = best.v = 0.0; best.prim = 0; best.aux = 0; best.kind = 0;
     unsigned long long ph = PH_T();
 #ifndef RT_NO_UNI  // ablation build: per-lane flat loads of the plane records
@@ -510,7 +594,13 @@ RT_D void shapes_closest(const DevScene& S, V3 o, V3 d, const Rcp3& rc, bool rfa
     }
     PH_ADD(kPhPlanes, ph);
     ph = PH_T();
-    {
+    if (SLT && uni_u32(S.slt_mask)) {
+        bool bv; double t = 0.0; uint32_t p = 0, aux = 0;
+        boxes_slt<ST>(S, o, d, rc, rfast, pend, C, bv, t, p, aux, *impact);
+        if (bv && (!best.valid || t < best.t)) {
+            best.valid = true; best.t = t; best.prim = p; best.aux = aux; best.kind = 1;
+        }
+    } else {
         double t, u, v; uint32_t p, aux = 0;
         if (bvh_closest_sel<1, ST, TF>(S.boxes, rfast, o, d, rc, stk, C, t, u, v, p, aux) && (!best.valid || t < best.t)) {
             best.valid = true; best.t = t; best.prim = p; best.aux = aux; best.kind = 1;
@@ -545,13 +635,13 @@ RT_D bool intersect_tail(const DevScene& S, const Cand& best, V3 o, V3 d, Cnt<ST
     C.shaded();
     return true;
 }
-template <bool ST, class Stk>
+template <bool ST, class Stk, bool SLT = false>
 RT_D bool scene_intersect(const DevScene& S, V3 o, V3 d, Stk& stk, Cnt<ST>& C, Hit& out, uint32_t& mat,
-                          int32_t& gid) {
+                          int32_t& gid, bool pend = false, double* impact = nullptr) {
     const Rcp3 rc = make_rcp3(d);
     const bool rfast = ray_fast(o, rc);
     Cand best;
-    shapes_closest<ST, false>(S, o, d, rc, rfast, stk, C, best);
+    shapes_closest<ST, false, Stk, SLT>(S, o, d, rc, rfast, stk, C, best, pend, impact);
     const unsigned long long ph = PH_T();
     double t, u = 0.0, v = 0.0; uint32_t p = 0, aux = 0;
     const bool th = bvh_closest_sel<3, ST>(S.tris, rfast, o, d, rc, stk, C, t, u, v, p, aux);
@@ -702,7 +792,8 @@ RT_D double light_pdf(const DevScene& S, V3 pos, V3 dir, Stk& stk, Cnt<ST>& C) {
     C.lq();
     uint32_t nh = 0;
     double impact = lights_impact<ST>(S, pos + dir * kEpsilon, dir, stk, C, nh);
-    return impact / (double)S.n_lights;
+    const uint32_t nl = S.n_lights;  // x / 1 == x exactly: skip the division sequence for one light
+    return nl == 1u ? impact : impact / (double)nl;
 }
 
 // ------------------------------------------------------------ samplers ----
@@ -737,8 +828,10 @@ RT_D V3 uniform_on_box(V3 s, Rng& r, const Scales& sc) {  // ray_sampler.rs:142-
     else p = v3(u1, u2, sign);
     return mul(p, s);
 }
-RT_D V3 light_sample(const DevScene& S, V3 pos, Rng& r, const Scales& sc) {  // ray_sampler.rs:101-130
-    uint64_t index = gen_index(r, S.n_lights, S.light_zone);
+RT_D V3 light_point(const DevScene& S, V3 pos, Rng& r, const Scales& sc) {  // ray_sampler.rs:101-129
+    // a one-element range needs no draw (the result is 0 either way; oracle.c gen_range_usize)
+    const uint32_t nl = uni_u32(S.n_lights);
+    uint64_t index = nl == 1u ? 0 : gen_index(r, nl, S.light_zone);
     rng_top_up(r);
     const uint32_t nb = S.lboxes.n_prims, ne = S.lells.n_prims;
     V3 world;
@@ -757,7 +850,10 @@ RT_D V3 light_sample(const DevScene& S, V3 pos, Rng& r, const Scales& sc) {  // 
         if (u + v > 1.0) { u = 1.0 - u; v = 1.0 - v; }
         world = (load3(t.ba) * u + load3(t.ca) * v) + load3(t.a);
     }
-    return normalize(world - pos);
+    return world;
+}
+RT_D V3 light_sample(const DevScene& S, V3 pos, Rng& r, const Scales& sc) {  // ray_sampler.rs:101-130
+    return normalize(light_point(S, pos, r, sc) - pos);
 }
 
 // --------------------------------------------------------- integrator ----
@@ -767,6 +863,12 @@ struct PathState {
     V3 o, d;       // current ray
     V3 T;          // throughput
     V3 L;          // radiance of this path so far
+    // a diffuse bounce whose light pdf comes with this segment's box tests
+    // (boxes_slt): its cos(dir, n), cosine pdf and material; T is updated once
+    // the pdf is known, before anything reads it
+    bool pend;
+    double pcs, pcos;
+    uint32_t pmat;
 };
 
 // The closest-hit query of one segment, held across path-loop trips while the
@@ -794,10 +896,10 @@ RT_D void segment_begin(const DevScene& S, const PathState& ps, Stk& stk, Cnt<ST
 // One segment of raytrace_impl (raytrace.rs:12-60) in throughput form, from
 // the closest-hit result on.  Returns true when the path continues with the
 // updated ray.
-template <bool ST, class Stk>
+template <bool ST, class Stk, bool SLT = false>
 RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, PathState& ps, Rng& rng,
                         Stk& stk, Cnt<ST>& C, bool hit, const Hit& h, uint32_t mat, int32_t gid,
-                        int32_t& hit_gid) {
+                        int32_t& hit_gid, bool more = false) {
     if (!hit) {
         hit_gid = RT_HIT_MISS;
         ps.L = ps.L + mul(ps.T, load3(P.bg));
@@ -814,16 +916,35 @@ RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, P
         V3 pos = o + d * h.t;
         const bool empty = S.n_lights == 0;
         V3 dir;
-        const bool by_cosine = empty || gen_bool(rng, 0.5);  // Mix::sample (ray_sampler.rs:87-93)
+        const bool by_cosine = empty || gen_half(rng);  // Mix::sample (ray_sampler.rs:87-93)
         rng_top_up(rng);
-        if (by_cosine) dir = cosine_sample(h.ns, rng);
-        else {
+        // both samplers end in normalize(w): one call after the branches join
+        V3 sw;
+        bool degen = false;
+        if (by_cosine) {
+            sw = uniform_on_sphere(rng) + h.ns;  // cosine_sample (ray_sampler.rs:69-76)
+            const double eps = kEpsilon * 16.0;
+            degen = fabs(sw.x) <= eps && fabs(sw.y) <= eps && fabs(sw.z) <= eps;
+        } else {
             const unsigned long long ph1 = PH_T();
-            dir = light_sample(S, pos, rng, sc);
+            sw = light_point(S, pos, rng, sc) - pos;
             PH_ADDW(kPhLightSample, ph1);
         }
+        dir = degen ? h.ns : normalize(sw);
         const double cs = dot(dir, h.ns);
         if (cs <= 0.0) return false;
+        if (SLT && more && uni_u32(S.slt_mask)) {
+            // the light query's ray is the next segment's: defer the pdf to its box
+            // tests.  cosine_pdf = cs / pi here (cs > 0); above 2^-1000 the Mix pdf
+            // (cos + light) / 2 cannot be 0, so the path surely continues.
+            const double cp = cosine_pdf(h.ns, dir);
+            if (cp > 0x1p-1000) {
+                ps.pend = true; ps.pcs = cs; ps.pcos = cp; ps.pmat = mat;
+                ps.o = pos + dir * kEpsilon;
+                ps.d = dir;
+                return true;
+            }
+        }
         double lp = 0.0;
         if (!empty) {
             const unsigned long long ph2 = PH_T();
@@ -887,13 +1008,24 @@ RT_D bool segment_end(const DevScene& S, const KParams& P, const Scales& sc, Pat
 // the fused form: one whole segment (scene_intersect to completion, then shade)
 template <bool ST, class Stk>
 RT_D bool segment(const DevScene& S, const KParams& P, const Scales& sc, PathState& ps, Rng& rng, Stk& stk,
-                  Cnt<ST>& C, int32_t& hit_gid) {
+                  Cnt<ST>& C, int32_t& hit_gid, bool more) {
     Hit h; uint32_t mat; int32_t gid;
     C.segment();
     const unsigned long long ph0 = PH_T();
-    const bool hit = scene_intersect<ST>(S, ps.o, ps.d, stk, C, h, mat, gid);
+    double impact = 0.0;
+    const bool hit = scene_intersect<ST, Stk, true>(S, ps.o, ps.d, stk, C, h, mat, gid, ps.pend, &impact);
+    if (ps.pend) {  // the previous bounce's Mix pdf and weight (raytrace.rs:26-33, ray_sampler.rs:95-97)
+        const uint32_t nl = S.n_lights;
+        const double lp = nl == 1u ? impact : impact / (double)nl;
+        const double pdf = (ps.pcos + lp) / 2.0;
+        const V3 col = load3(S.mats[ps.pmat].color);
+        const V3 w = v3(((ps.pcs * col.x) / kPi) / pdf, ((ps.pcs * col.y) / kPi) / pdf,
+                        ((ps.pcs * col.z) / kPi) / pdf);
+        ps.T = mul(ps.T, w);
+        ps.pend = false;
+    }
     PH_ADDW(kPhIntersect, ph0);
-    return segment_shade<ST>(S, P, sc, ps, rng, stk, C, hit, h, mat, gid, hit_gid);
+    return segment_shade<ST, Stk, true>(S, P, sc, ps, rng, stk, C, hit, h, mat, gid, hit_gid, more);
 }
 
 template <bool ST>
@@ -1045,6 +1177,7 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
                         ps.d = normalize(dir);
                         ps.T = v3(1.0, 1.0, 1.0);
                         ps.L = v3(0.0, 0.0, 0.0);
+                        ps.pend = false;
                         b = 0;
                         busy = true;
                         C.path();
@@ -1100,7 +1233,7 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
                 if (b < depth) {
                     int32_t g;
                     const unsigned long long ph_s = PH_T();
-                    cont = segment<ST>(S, P, sc, ps, rng, stk, C, g);
+                    cont = segment<ST>(S, P, sc, ps, rng, stk, C, g, b + 1 < depth);
                     PH_ADDW(kPhSegment, ph_s);
                     if (HIT) hit_ids[(pixel * P.spp + s) * depth + b] = g;
                     ++b;
@@ -1287,8 +1420,16 @@ using PathFn = void (*)(DevScene, KParams, const DevScene*, const KParams*, doub
                         unsigned long long*, uint32_t*, double*, uint32_t*, double*);
 template <bool ST, bool HIT>
 PathFn path_fn_r(uint32_t waves, bool resume) {
+#ifdef RT_ONLY_C2  // experiment builds (tools/variants.py): only the C2 instance, 4x faster to compile
+    (void)waves; (void)resume;
+    return path_kernel<ST, HIT, 3, false>;
+#elif defined(RT_ONLY_C3)  // ... only the C3 instance
+    (void)waves; (void)resume;
+    return path_kernel<ST, HIT, 4, true>;
+#else
     if (waves == 4) return resume ? path_kernel<ST, HIT, 4, true> : path_kernel<ST, HIT, 4, false>;
     return resume ? path_kernel<ST, HIT, 3, true> : path_kernel<ST, HIT, 3, false>;
+#endif
 }
 PathFn path_fn(bool stats, bool hits, uint32_t waves, bool resume) {
     if (stats) return hits ? path_fn_r<true, true>(waves, resume) : path_fn_r<true, false>(waves, resume);

@@ -98,6 +98,13 @@ struct DevScene {
     // (side = aux bit0), box in BVH order [n][aux & 7][3] (face dim, sign bit)
     const double* plane_nrm;
     const double* box_nrm;
+    // Shared light tests (render.hip boxes_slt): bit i set <=> scene box i (BVH
+    // order) is the next light box of lboxes.  Nonzero only when every light is
+    // a box, both box BVHs are single leaves and the light copies are the scene
+    // records selected by the mask, in order: the light pdf of a diffuse bounce
+    // then comes from the next segment's own box tests (same ray, same records).
+    uint32_t slt_mask;
+    uint32_t _pad2;
 };
 
 }  // namespace rt

@@ -178,6 +178,11 @@ typedef struct rt_scene_info {
     double   build_ms;           /* host BVH build                                */
     double   upload_ms;          /* H2D copy                                      */
     uint64_t device_bytes;
+    /* bit i: scene box i (BVH order) doubles as the next light box, so the light
+       pdf of a diffuse bounce comes from the next segment's box tests (DESIGN.md
+       §4 "shared light tests"); 0 = separate light queries */
+    uint32_t shared_light_mask;
+    uint32_t reserved;
 } rt_scene_info;
 int rt_scene_get_info(const rt_scene* scene, rt_scene_info* out);
 

@@ -801,6 +801,11 @@ static int32_t gen_range_i32_0_1(Rng* r) { /* UniformInt<i32>::sample_single_inc
         if (lo <= zone) return (int32_t)hi;
     }
 }
+/* Bernoulli(0.5) from ONE word: P(w < 2^31) = 1/2 exactly, the distribution of
+   gen_bool(0.5) (whose u64 draw this stream layout does not spend).  With one
+   word for the Mix coin (and none for a single light's index), every diffuse
+   sampler fits the two Philox blocks the device generates before it branches. */
+static inline int gen_half(Rng* r) { return next_u32(r) < 0x80000000u; }
 static int gen_bool(Rng* r, double p) { /* Bernoulli::new(p) + sample */
     if (p == 1.0) return 1; /* ALWAYS_TRUE: no draw */
     uint64_t p_int = (p >= 0.0 && p < 1.0) ? (uint64_t)(p * 18446744073709551616.0) : 0; /* NaN: reference panics */
@@ -839,7 +844,9 @@ static V3 uniform_on_box(V3 s, Rng* r) { /* :142-157 */
 }
 static V3 light_sample(const oracle_scene* s, V3 pos, Rng* r) { /* :101-130 */
     uint64_t len = s->lells.n + s->lboxes.n + s->ltris.n;
-    uint64_t index = gen_range_usize(r, len);
+    /* gen_range(0..1) is 0 whatever it draws: no draw for a single light (a choice of
+       this build's stream layout, like rng_align; the distribution is the same) */
+    uint64_t index = len == 1 ? 0 : gen_range_usize(r, len);
     V3 world;
     if (index < s->lboxes.n) {
         const Shape* l = &s->lboxes.s[index];
@@ -901,7 +908,7 @@ static int diffuse_sample(Ctx* x, V3 pos, V3 n, V3* dir_out, double* pdf_out) {
     V3 dir;
     int empty = lights_empty(s);
     if (empty) dir = cosine_sample(n, x->rng);
-    else dir = gen_bool(x->rng, 0.5) ? cosine_sample(n, x->rng) : light_sample(s, pos, x->rng); /* Mix::sample :87-93 */
+    else dir = gen_half(x->rng) ? cosine_sample(n, x->rng) : light_sample(s, pos, x->rng); /* Mix::sample :87-93 */
     if (vdot(dir, n) <= 0.0) return 0;
     double pdf = empty ? cosine_pdf(n, dir)
                        : (cosine_pdf(n, dir) + light_pdf(s, pos, dir, x->c)) / 2.0; /* Mix::pdf :95-97 */
@@ -1178,6 +1185,7 @@ void oracle_sampler_draws(uint64_t seed, uint64_t pixel, uint32_t sample, int ki
         case 4: v.x = (double)gen_bool(&r, arg[0]); break;
         case 5: v.x = gen_range_incl_f64(&r, arg[0], arg[1]); break;
         case 6: v.x = gen_range_f64(&r, arg[0], arg[1]); break;
+        case 7: v.x = (double)gen_half(&r); break;
         default: break;
         }
         vst(out + 3 * i, v);

@@ -101,6 +101,36 @@ def test_kitchen_sink(sink):
     _compare(g, o, params)
 
 
+@pytest.fixture(scope="module")
+def box_lights(rt, orc, scene_text):
+    desc, params = rt.parse_scene(scene_text("box_lights.txt"))
+    return desc, params, rt.Scene(desc), orc.OracleScene(desc)
+
+
+def test_shared_light_tests_cornell(cornell):
+    """Cornell's only light is a box in the single-leaf box BVH: its light pdf
+    comes from the next segment's box tests (boxes_slt), still bit-exact."""
+    desc, params, g, o = cornell
+    assert g.info()["shared_light_mask"] == 0b01  # the light box precedes the rotated box
+    _compare(g, o, params.replace(width=32, height=24, spp=4, ray_depth=12))
+
+
+@pytest.mark.parametrize("over", [dict(), dict(width=20, height=16, spp=3, ray_depth=30, seed=7),
+                                  dict(width=9, height=7, spp=5, ray_depth=2, seed=11)])
+def test_shared_light_tests_box_lights(box_lights, over):
+    """Two box lights (one rotated, one also diffuse) mixed with non-light boxes:
+    light pdfs from shared tests, several lights (index draws), rotated light
+    normals, deep and shallow paths — hit ids, radiance and counters exact."""
+    desc, params, g, o = box_lights
+    assert g.info()["shared_light_mask"] == 0b101
+    _compare(g, o, params.replace(**over))
+
+
+def test_no_shared_light_tests_with_other_lights(sink):
+    desc, params, g, o = sink
+    assert g.info()["shared_light_mask"] == 0  # ellipsoid and triangle lights: separate queries
+
+
 def test_kitchen_sink_deep(sink):
     desc, params, g, o = sink
     _compare(g, o, params.replace(width=24, height=20, spp=3, ray_depth=24, seed=99))

@@ -155,6 +155,7 @@ def test_samplers_geometry(orc):
     ("cornell.txt", dict(width=32, height=24, spp=4)),
     ("kitchen_sink.txt", {}),
     ("kitchen_sink.txt", dict(width=16, height=12, spp=3, ray_depth=30, seed=5)),
+    ("box_lights.txt", dict(width=16, height=12, spp=3)),
 ])
 def test_recursive_vs_iterative(rt, orc, scene_text, scene, over):
     desc, params = rt.parse_scene(scene_text(scene))
