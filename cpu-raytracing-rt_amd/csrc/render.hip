@@ -480,7 +480,11 @@ RT_D Hit materialise(const DevScene& S, const Cand& c, V3 o, V3 d, Quat& rot, ui
         V3 n = ell_normal(load_radii(s), mo, md, c.t);
         bool inside = (c.aux & 8u) != 0;
         if (inside) n = -n;
+        // both normals are this n, so with_rotated_normal's two rotate + normalize
+        // results are the same bits: computed once here (world = true)
+        n = normalize(rotate_fast(rot, is_identity(rot), n));
         h.ng = n; h.ns = n; h.inside = inside;
+        world = true;
     }
     return h;
 }
@@ -859,6 +863,17 @@ RT_D V3 light_sample(const DevScene& S, V3 pos, Rng& r, const Scales& sc) {  // 
 // --------------------------------------------------------- integrator ----
 RT_D double powi5(double x) { double x2 = x * x; return x * (x2 * x2); }
 
+// Throughput weight of a diffuse bounce, col * cos / pi / pdf (raytrace.rs:26-33),
+// as col * (cosine_pdf / pdf): cosine_pdf is cos / pi exactly as computed for the
+// Mix pdf (cos > 0 here), so one division replaces the six of the per-channel
+// form.  The weight only scales radiance — no random decision reads it — so hit
+// ids stay bit-exact and radiance moves by an ulp-level reassociation (oracle.c
+// raytrace_iter does the same; the recursive form is within rtol 1e-12).
+RT_D V3 diffuse_weight(V3 col, double cp, double pdf) {
+    const double f = cp / pdf;
+    return v3(col.x * f, col.y * f, col.z * f);
+}
+
 struct PathState {
     V3 o, d;       // current ray
     V3 T;          // throughput
@@ -867,7 +882,7 @@ struct PathState {
     // (boxes_slt): its cos(dir, n), cosine pdf and material; T is updated once
     // the pdf is known, before anything reads it
     bool pend;
-    double pcs, pcos;
+    double pcos;
     uint32_t pmat;
 };
 
@@ -939,7 +954,7 @@ RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, P
             // (cos + light) / 2 cannot be 0, so the path surely continues.
             const double cp = cosine_pdf(h.ns, dir);
             if (cp > 0x1p-1000) {
-                ps.pend = true; ps.pcs = cs; ps.pcos = cp; ps.pmat = mat;
+                ps.pend = true; ps.pcos = cp; ps.pmat = mat;
                 ps.o = pos + dir * kEpsilon;
                 ps.d = dir;
                 return true;
@@ -951,10 +966,10 @@ RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, P
             lp = light_pdf<ST>(S, pos, dir, stk, C);
             PH_ADDW(kPhLightPdf, ph2);
         }
-        double pdf = empty ? cosine_pdf(h.ns, dir) : (cosine_pdf(h.ns, dir) + lp) / 2.0;  // Mix::pdf
+        const double cp = cosine_pdf(h.ns, dir);
+        double pdf = empty ? cp : (cp + lp) / 2.0;  // Mix::pdf
         if (pdf == 0.0) return false;
-        V3 w = v3(((cs * col.x) / kPi) / pdf, ((cs * col.y) / kPi) / pdf, ((cs * col.z) / kPi) / pdf);
-        ps.T = mul(ps.T, w);
+        ps.T = mul(ps.T, diffuse_weight(col, cp, pdf));
         ps.o = pos + dir * kEpsilon;
         ps.d = dir;
         return true;
@@ -963,15 +978,14 @@ RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, P
     const V3 rdir = d - (h.ns * 2.0) * dot(h.ns, d);
     const V3 hp = o + d * h.t;
     if (m.kind == RT_MAT_DIELECTRIC) {  // :36-54
-        double n1 = 1.0, n2 = m.ior;
-        if (h.inside) { double t = n1; n1 = n2; n2 = t; }
-        const double k = n1 / n2;
+        // n1 / n2 and r0 are per-material constants (DevMaterial::k_out, r0)
+        const double k = h.inside ? m.ior : m.k_out;
         // refracted_ray (raytrace.rs:75-88)
         const double cos1 = -dot(h.ns, d);
         const double sin2 = k * sqrt(1.0 - cos1 * cos1);
         bool reflect = true;
         if (!(sin2 > 1.0)) {
-            const double r0 = ((n1 - n2) / (n1 + n2)) * ((n1 - n2) / (n1 + n2));  // powi(_, 2)
+            const double r0 = m.r0;  // ((n1 - n2) / (n1 + n2)).powi(2)
             const double power = r0 + (1.0 - r0) * powi5(1.0 + dot(d, h.ns));   // reflection_power
             double p = power;
             if (p < 0.0) p = 0.0;
@@ -1018,10 +1032,7 @@ RT_D bool segment(const DevScene& S, const KParams& P, const Scales& sc, PathSta
         const uint32_t nl = S.n_lights;
         const double lp = nl == 1u ? impact : impact / (double)nl;
         const double pdf = (ps.pcos + lp) / 2.0;
-        const V3 col = load3(S.mats[ps.pmat].color);
-        const V3 w = v3(((ps.pcs * col.x) / kPi) / pdf, ((ps.pcs * col.y) / kPi) / pdf,
-                        ((ps.pcs * col.z) / kPi) / pdf);
-        ps.T = mul(ps.T, w);
+        ps.T = mul(ps.T, diffuse_weight(load3(S.mats[ps.pmat].color), ps.pcos, pdf));
         ps.pend = false;
     }
     PH_ADDW(kPhIntersect, ph0);
@@ -1408,7 +1419,7 @@ __global__ void unpack_kernel(const double* __restrict__ g, double* __restrict__
 __global__ void fp64_probe_kernel(const double* a, const double* b, double* out, uint32_t n, int op) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    out[i] = op == 0 ? sqrt(a[i]) : a[i] / b[i];
+    out[i] = op == 0 ? sqrt(a[i]) : (op == 1 ? a[i] / b[i] : dev_quot(a[i], b[i], dev_rcp(b[i])));
 }
 
 // ------------------------------------------------------------- launch ----

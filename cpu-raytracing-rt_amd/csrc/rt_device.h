@@ -185,36 +185,55 @@ struct Cnt {
 };
 
 // ------------------------------------------------------ exact division ----
-// x / y correctly rounded from a precomputed r = RN(1/y): q0 = x*r, then two
-// FMA-residual corrections (Markstein: once q is within 1 ulp, q + (x - q*y)*r
-// rounds to RN(x/y); the first correction makes q0 faithful, the second
-// rounds).  The residuals x - q*y are exact (FMA) as long as nothing
-// under/overflows, which the exponent guard ensures: both |x| and |y| in
-// [2^-450, 2^451).  Outside it (incl. 0, inf, NaN, subnormals) the plain IEEE
-// division runs.  5 f64 ops instead of the ~10-op v_div_scale/v_rcp/v_div_fmas/
-// v_div_fixup sequence.  Checked bit-for-bit against x / y on 1.2e8 adversarial
-// pairs (tools/fastdiv_check.c) and by every parity test.
+// Two exact division forms besides the plain `x / y`:
+//
+// (1) The device's own division, split.  x / y compiles on gfx950 to
+//       d = v_div_scale(y), r = v_rcp(d), two Newton steps r += r * (1 - d*r),
+//       n = v_div_scale(x), q = n*r, rem = fma(-d, q, n),
+//       v_div_fmas(rem, r, q), v_div_fixup
+//     (render.hip ISA).  When neither operand needs div_scale's rescaling,
+//     div_scale returns its operand, div_fmas is fma(rem, r, q) and div_fixup
+//     passes a finite normal quotient through — so the sequence splits into a
+//     per-divisor reciprocal part (dev_rcp: rcp + 4 FMAs) and a per-dividend
+//     quotient part (dev_quot: mul + 2 FMAs) with the SAME bits as x / y.  No
+//     rescaling happens for |y| in [2^-360, 2^360] (dir_ok) and |x| in
+//     [2^-500, 2^402]: the exponent gap stays below 768, the quotient is
+//     normal and the dividend's exponent far above the tiny-numerator case.
+//     A ray's 3 reciprocals then serve every slab and shape quotient of the
+//     ray at 3 ops each (instead of 5 with RN(1/y) below, or ~11 for x / y).
+//     Checked bit for bit against the host's x / y on random and adversarial
+//     pairs of the range (tests/test_gpu_parity.py test_dev_quot_matches_host).
+//
+// (2) fdiv_fast: x / y correctly rounded from r = RN(1/y) (a host constant,
+//     e.g. an ellipsoid's 1/r): q0 = x*r, then two FMA-residual corrections
+//     (Markstein: once q is within 1 ulp, q + (x - q*y)*r rounds to RN(x/y)).
+//     Exact for |x|, |y| in [2^-450, 2^451) (fd_ok: the residuals stay exact);
+//     checked on 1.2e8 adversarial pairs (tools/fastdiv_check.c).
 RT_D bool fd_ok(double v) {
     return (((uint32_t)((uint64_t)__double_as_longlong(v) >> 52) & 0x7ffu) - 573u) < 901u;
 }
-RT_D double fdiv_r(double x, double y, double r, bool yok) {
-#ifndef RT_FASTDIV  // opt-in: measured slower than the hardware sequence in the megakernel
-    return x / y;
-#endif
-    if (yok && fd_ok(x)) {
-        const double q0 = x * r;
-        const double e0 = fma(-q0, y, x);
-        const double q1 = fma(e0, r, q0);
-        const double e1 = fma(-q1, y, x);
-        return fma(e1, r, q1);
-    }
-    return x / y;
+// |d| in [2^-360, 2^360]: a ray direction component whose quotients may take dev_quot
+RT_D bool dir_ok(double v) {
+    return (((uint32_t)((uint64_t)__double_as_longlong(v) >> 52) & 0x7ffu) - 663u) < 721u;
 }
-// Unguarded form for slab tests whose operands are proven in range up front
-// (scene boxes and ray origin in kCoordLo..kCoordHi or zero, |d| per fd_ok):
-// then x = min - o is 0 or a multiple of 2^-449 below 2^401, so fd_ok(x)
-// always holds except x == +-0, where the result differs from x / y at most in
-// the sign of zero — which no comparison of the slab test observes.
+RT_D double dev_rcp(double y) {
+    double r = __builtin_amdgcn_rcp(y);
+    double e = fma(-y, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-y, r, 1.0);
+    return fma(r, e, r);
+}
+RT_D double dev_quot(double x, double y, double r) {
+    const double q = x * r;
+    const double rem = fma(-y, q, x);
+    return fma(rem, r, q);
+}
+// dev_quot that also returns x / y's signed zero for x == +-0 (x * r has the
+// sign sign(x) ^ sign(y), as x / y does)
+RT_D double dev_quotz(double x, double y, double r) {
+    const double q = dev_quot(x, y, r);
+    return x == 0.0 ? x * r : q;
+}
 RT_D double fdiv_fast(double x, double y, double r) {
     const double q0 = x * r;
     const double e0 = fma(-q0, y, x);
@@ -222,25 +241,20 @@ RT_D double fdiv_fast(double x, double y, double r) {
     const double e1 = fma(-q1, y, x);
     return fma(e1, r, q1);
 }
-// fdiv_fast that also returns x / y's signed zero for x == +-0 (x * r has the
-// sign sign(x) ^ sign(y), as x / y does): exact for every x in the range.
-RT_D double fdiv_fastz(double x, double y, double r) {
-    const double q = fdiv_fast(x, y, r);
-    return x == 0.0 ? x * r : q;
-}
-constexpr double kInvPi = 1.0 / kPi;  // RN(1/pi), folded exactly at compile time
-RT_D double div_pi(double x) { return fdiv_r(x, kPi, kInvPi, true); }
 
-// per-axis reciprocals of a ray direction (shared by every slab test of a ray)
+// per-axis reciprocals of a ray direction (shared by every slab test of a ray):
+// dev_rcp(d) for dev_quot; ok bit i <=> dir_ok(d[i])
 struct Rcp3 {
     V3 r;
-    uint32_t ok;  // bit i: axis i usable by fdiv_r
+    uint32_t ok;
 };
 RT_D Rcp3 make_rcp3(V3 d) {
-    return Rcp3{v3(1.0 / d.x, 1.0 / d.y, 1.0 / d.z),
-                (fd_ok(d.x) ? 1u : 0u) | (fd_ok(d.y) ? 2u : 0u) | (fd_ok(d.z) ? 4u : 0u)};
+    return Rcp3{v3(dev_rcp(d.x), dev_rcp(d.y), dev_rcp(d.z)),
+                (dir_ok(d.x) ? 1u : 0u) | (dir_ok(d.y) ? 2u : 0u) | (dir_ok(d.z) ? 4u : 0u)};
 }
-// a ray whose slab tests may take fdiv_fast (given DevBvh::fast boxes)
+// a ray whose slab and shape quotients may take dev_quot (given DevBvh::fast
+// boxes / kShapeFast shapes): coordinates 0 or in [2^-397, 2^400], so every
+// dividend min - o is 0 or in [2^-449, 2^401]
 RT_D bool ray_fast(V3 o, const Rcp3& rc) {
     return rc.ok == 7u && coord_fast(o.x) && coord_fast(o.y) && coord_fast(o.z);
 }
@@ -272,9 +286,9 @@ RT_D double safe_max(double a, double b) {
 //   * so hit <=> t_near <= t_far && 0 <= t_far, and t = max(t_near, 0).
 // (The host sets DevBvh::fast only when every box has min <= max per axis.)
 RT_D bool aabb_hit_fast(V3 mn, V3 mx, V3 o, const Rcp3& rc, V3 d, double& t) {
-    const double ax = fdiv_fast(mn.x - o.x, d.x, rc.r.x), bx = fdiv_fast(mx.x - o.x, d.x, rc.r.x);
-    const double ay = fdiv_fast(mn.y - o.y, d.y, rc.r.y), by = fdiv_fast(mx.y - o.y, d.y, rc.r.y);
-    const double az = fdiv_fast(mn.z - o.z, d.z, rc.r.z), bz = fdiv_fast(mx.z - o.z, d.z, rc.r.z);
+    const double ax = dev_quot(mn.x - o.x, d.x, rc.r.x), bx = dev_quot(mx.x - o.x, d.x, rc.r.x);
+    const double ay = dev_quot(mn.y - o.y, d.y, rc.r.y), by = dev_quot(mx.y - o.y, d.y, rc.r.y);
+    const double az = dev_quot(mn.z - o.z, d.z, rc.r.z), bz = dev_quot(mx.z - o.z, d.z, rc.r.z);
     const double tn = __builtin_fmax(__builtin_fmax(__builtin_fmin(ax, bx), __builtin_fmin(ay, by)),
                                      __builtin_fmin(az, bz));
     const double tf = __builtin_fmin(__builtin_fmin(__builtin_fmax(ax, bx), __builtin_fmax(ay, by)),
@@ -296,16 +310,13 @@ RT_D bool aabb_hit(V3 mn, V3 mx, V3 o, V3 d, const Rcp3& rc, double& t) {
     }
     V3 tmin, tmax;
     if (FAST) {
-        tmin = v3(fdiv_fast(mn.x - o.x, d.x, rc.r.x), fdiv_fast(mn.y - o.y, d.y, rc.r.y),
-                  fdiv_fast(mn.z - o.z, d.z, rc.r.z));
-        tmax = v3(fdiv_fast(mx.x - o.x, d.x, rc.r.x), fdiv_fast(mx.y - o.y, d.y, rc.r.y),
-                  fdiv_fast(mx.z - o.z, d.z, rc.r.z));
+        tmin = v3(dev_quot(mn.x - o.x, d.x, rc.r.x), dev_quot(mn.y - o.y, d.y, rc.r.y),
+                  dev_quot(mn.z - o.z, d.z, rc.r.z));
+        tmax = v3(dev_quot(mx.x - o.x, d.x, rc.r.x), dev_quot(mx.y - o.y, d.y, rc.r.y),
+                  dev_quot(mx.z - o.z, d.z, rc.r.z));
     } else {
-        const bool okx = rc.ok & 1u, oky = rc.ok & 2u, okz = rc.ok & 4u;
-        tmin = v3(fdiv_r(mn.x - o.x, d.x, rc.r.x, okx), fdiv_r(mn.y - o.y, d.y, rc.r.y, oky),
-                  fdiv_r(mn.z - o.z, d.z, rc.r.z, okz));
-        tmax = v3(fdiv_r(mx.x - o.x, d.x, rc.r.x, okx), fdiv_r(mx.y - o.y, d.y, rc.r.y, oky),
-                  fdiv_r(mx.z - o.z, d.z, rc.r.z, okz));
+        tmin = div(mn - o, d);
+        tmax = div(mx - o, d);
     }
     double t1x = safe_min(tmin.x, tmax.x), t1y = safe_min(tmin.y, tmax.y), t1z = safe_min(tmin.z, tmax.z);
     double t2x = safe_max(tmin.x, tmax.x), t2y = safe_max(tmin.y, tmax.y), t2z = safe_max(tmin.z, tmax.z);
@@ -372,7 +383,7 @@ RT_D bool plane_t(V3 n, V3 o, V3 d, double& t, uint32_t& aux) {
 
 // intersect_box_coef (box.rs:75-115). Entry/exit as (t, sign, dim).
 struct Bpi { double t; double sign; int dim; };
-// FD: shape_fast holds (d has no zero component; every quotient exact by fdiv_fastz)
+// FD: shape_fast holds (d has no zero component; every quotient exact by dev_quotz)
 template <bool FD = false>
 RT_D int box_coef(V3 s, V3 o, V3 d, const Rcp3& rc, Bpi& en, Bpi& ex) {
     bool have = false;
@@ -382,9 +393,8 @@ RT_D int box_coef(V3 s, V3 o, V3 d, const Rcp3& rc, Bpi& en, Bpi& ex) {
         if (!FD && di == 0.0 && si < fabs(oi)) return 0;
         if (!FD && di == 0.0) continue;
         const double ri = comp(rc.r, i);
-        const bool ok = (rc.ok >> i) & 1u;
-        double t1 = FD ? fdiv_fastz(si - oi, di, ri) : fdiv_r(si - oi, di, ri, ok);
-        double t2 = FD ? fdiv_fastz(-si - oi, di, ri) : fdiv_r(-si - oi, di, ri, ok);
+        double t1 = FD ? dev_quotz(si - oi, di, ri) : (si - oi) / di;
+        double t2 = FD ? dev_quotz(-si - oi, di, ri) : (-si - oi) / di;
         double a, b, nrm;
         if (t1 < t2) { a = t1; b = t2; nrm = 1.0; } else { a = t2; b = t1; nrm = -1.0; }
         if (!have) { en = Bpi{a, nrm, i}; ex = Bpi{b, nrm, i}; have = true; }
@@ -419,15 +429,10 @@ RT_D V3 aux_box_normal(uint32_t aux) {
 // Ellipsoid radii with their host-precomputed reciprocals (DevShape::aux).
 struct Radii {
     V3 r, inv;
-    uint32_t ok;
 };
-RT_D Radii load_radii(const DevShape& s) {
-    V3 r = load3(s.shape);
-    return Radii{r, load3(s.aux), (fd_ok(r.x) ? 1u : 0u) | (fd_ok(r.y) ? 2u : 0u) | (fd_ok(r.z) ? 4u : 0u)};
-}
+RT_D Radii load_radii(const DevShape& s) { return Radii{load3(s.shape), load3(s.aux)}; }
 RT_D V3 div_radii(V3 v, const Radii& R) {  // v.div_element_wise(r)
-    return v3(fdiv_r(v.x, R.r.x, R.inv.x, R.ok & 1u), fdiv_r(v.y, R.r.y, R.inv.y, R.ok & 2u),
-              fdiv_r(v.z, R.r.z, R.inv.z, R.ok & 4u));
+    return div(v, R.r);
 }
 
 // intersect_ellipsoid_coef (ellipsoid.rs:49-76).  FD: shape_fast holds (o
@@ -445,9 +450,7 @@ RT_D int ell_coef(const Radii& R, V3 o, V3 d, double& t1o, double& t2o) {
     double disc = b * b - a * (c - 1.0);
     if (disc < 0.0) return 0;
     double ds = sqrt(disc);
-    const double ra = 1.0 / a;
-    const bool aok = fd_ok(a);
-    double t1 = fdiv_r(-b + ds, a, ra, aok), t2 = fdiv_r(-b - ds, a, ra, aok);
+    double t1 = (-b + ds) / a, t2 = (-b - ds) / a;
     if (t2 < t1) { double tmp = t1; t1 = t2; t2 = tmp; }
     t1o = t1; t2o = t2;
     if (0.0 <= t1) return 2;
@@ -465,9 +468,7 @@ RT_D bool tri_uvt(const DevTri& tr, V3 o, V3 d, double& u, double& v, double& t)
     double det = m0.x * (m1.y * m2.z - m2.y * m1.z) - m1.x * (m0.y * m2.z - m2.y * m0.z) +
                  m2.x * (m0.y * m1.z - m1.y * m0.z);
     if (fabs(det) < 1e-11) return false;
-    const double rd = 1.0 / det;
-    const bool ok = fd_ok(det);
-    auto dv = [&](V3 c) { return v3(fdiv_r(c.x, det, rd, ok), fdiv_r(c.y, det, rd, ok), fdiv_r(c.z, det, rd, ok)); };
+    auto dv = [&](V3 c) { return c / det; };
     V3 x0 = dv(cross(m1, m2)), x1 = dv(cross(m2, m0)), x2 = dv(cross(m0, m1));
     V3 w = o - load3(tr.a);
     double uu = dot(x0, w), vv = dot(x1, w), tt = dot(x2, w);

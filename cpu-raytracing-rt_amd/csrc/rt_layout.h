@@ -37,7 +37,7 @@ struct alignas(16) DevShape {  // Primitive<T> hot part (scene.rs:20-27)
     double pos[3];
     double rot[4];             // (s, x, y, z)
     // host-precomputed constants (same IEEE ops as the device would do):
-    //   ellipsoid: aux = RN(1/r) per axis (exact reciprocal division, RT_FASTDIV)
+    //   ellipsoid: aux = RN(1/r) per axis (for rt_device.h fdiv_fast)
     //   box:       aux[0] = 1/sum/8 (intersection_probability.rs:15-23)
     double aux[3];
     // kShapeFast: identity rotation, position (and box sizes / plane normal /
@@ -64,6 +64,11 @@ struct DevMaterial {           // Metadata (scene.rs:13-18)
     uint32_t kind, pad;
     double ior;
     double color[3], emission[3];
+    // dielectric constants of raytrace.rs:36-54, host-computed with the same IEEE
+    // ops: k_out = 1 / ior (entering; inside, n1 / n2 = ior / 1 = ior exactly) and
+    // r0 = ((n1 - n2) / (n1 + n2))^2 of reflection_power (raytrace.rs:62-65), the
+    // same bits for both sides (the quotient only changes sign)
+    double k_out, r0;
 };
 
 struct DevBvh {

@@ -383,6 +383,9 @@ std::string build_scene(const rt_scene_desc& d, HostScene& out) {
         if (m.kind > RT_MAT_DIELECTRIC) return "bad material kind";
         DevMaterial dm;
         dm.kind = m.kind; dm.pad = 0; dm.ior = m.ior;
+        const double q = (1.0 - m.ior) / (1.0 + m.ior);
+        dm.k_out = 1.0 / m.ior;
+        dm.r0 = q * q;
         for (int k = 0; k < 3; ++k) { dm.color[k] = m.color[k]; dm.emission[k] = m.emission[k]; }
         out.mats[i] = dm;
     }

@@ -296,8 +296,9 @@ const char* rt_last_error(void);
 int rt_api_version(void);
 /* Number of visible HIP devices (0 when none); never fails. */
 int rt_device_count(void);
-/* Diagnostic: device f64 sqrt (op 0) or a/b (op 1) for n values, to check that
-   the device rounds like the host (the bit-exact parity premise). */
+/* Diagnostic: device f64 sqrt (op 0), a/b (op 1) or the kernels' split division
+   dev_quot(a, b, dev_rcp(b)) (op 2, rt_device.h) for n values, to check that the
+   device rounds like the host (the bit-exact parity premise). */
 int rt_probe_fp64(int op, const double* a, const double* b, uint32_t n, double* out);
 
 #ifdef __cplusplus

@@ -980,8 +980,11 @@ static V3 raytrace_iter(Ctx* x, V3 o, V3 d) {
             V3 pos = vadd(o, vscale(d, h->t));
             V3 dir; double pdf;
             if (!diffuse_sample(x, pos, h->ns, &dir, &pdf)) break;
-            double cs = vdot(dir, h->ns);
-            V3 w = v3(((cs * col.x) / R_PI) / pdf, ((cs * col.y) / R_PI) / pdf, ((cs * col.z) / R_PI) / pdf);
+            /* col * cos / pi / pdf reassociated as col * (cosine_pdf / pdf), the device's
+               one-division form (render.hip diffuse_weight): radiance only, so hit ids are
+               unchanged and the recursive form above stays within rtol 1e-12 */
+            double f = cosine_pdf(h->ns, dir) / pdf;
+            V3 w = v3(col.x * f, col.y * f, col.z * f);
             T = vmul(T, w);
             o = vadd(pos, vscale(dir, R_EPSILON));
             d = dir;

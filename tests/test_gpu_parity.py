@@ -64,6 +64,46 @@ def test_fp64_rounding_matches_host(rt):
     assert np.array_equal(rt.probe_fp64(1, a, b), a / b)
 
 
+def _split_division_pairs(n, seed):
+    """Dividend/divisor pairs of dev_quot's range (rt_device.h): |x| in [2^-500, 2^402],
+    |y| in [2^-360, 2^360], random signs; random mantissas plus the adversarial ones
+    (all-ones, 1 + ulp, powers of two) and quotients near rounding ties."""
+    rng = np.random.default_rng(seed)
+
+    def dbl(mant, exp, sign):
+        return np.ldexp(1.0 + mant * 2.0 ** -52, exp) * sign
+
+    sx = rng.choice([-1.0, 1.0], n)
+    sy = rng.choice([-1.0, 1.0], n)
+    ex = rng.integers(-500, 402, n)
+    ey = rng.integers(-360, 360, n)
+    mx = rng.integers(0, 2 ** 52, n, dtype=np.uint64).astype(np.float64)
+    my = rng.integers(0, 2 ** 52, n, dtype=np.uint64).astype(np.float64)
+    special = np.array([0.0, 1.0, 2.0 ** 52 - 1, 2.0 ** 52 - 2, 2.0 ** 51, 2.0 ** 51 - 1, 1.0 + 2.0 ** 51])
+    k = n // 4
+    my[:k] = special[rng.integers(0, len(special), k)]
+    mx[k:2 * k] = special[rng.integers(0, len(special), k)]
+    x, y = dbl(mx, ex, sx), dbl(my, ey, sy)
+    # x = y * q (rounded) for short q: exact or near-tie quotients
+    q = rng.integers(1, 2 ** 20, k).astype(np.float64) * 2.0 ** rng.integers(-30, 30, k)
+    x[2 * k:3 * k] = y[2 * k:3 * k] * q
+    x[3 * k:] = np.nextafter(y[3 * k:] * q[: n - 3 * k], np.inf)
+    ok = (np.abs(x) >= 2.0 ** -500) & (np.abs(x) <= 2.0 ** 402)
+    return x[ok], y[ok]
+
+
+def test_dev_quot_matches_host(rt):
+    """The kernels' split division (dev_rcp once per divisor, dev_quot per dividend) is
+    the device's own division without its rescaling steps: inside its range it must give
+    the host's correctly rounded x / y bit for bit (rt_device.h)."""
+    for seed in range(4):
+        x, y = _split_division_pairs(1 << 20, seed)
+        got = rt.probe_fp64(2, x, y)
+        bad = np.flatnonzero(got.view(np.uint64) != (x / y).view(np.uint64))
+        assert bad.size == 0, [(x[i], y[i], got[i], x[i] / y[i]) for i in bad[:5]]
+        assert np.array_equal(rt.probe_fp64(1, x, y), x / y)
+
+
 def test_cornell_small(cornell):
     desc, params, g, o = cornell
     _compare(g, o, params.replace(width=48, height=40, spp=4))
