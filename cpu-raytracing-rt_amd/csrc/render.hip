@@ -1060,6 +1060,19 @@ RT_D void wave_flush(const Cnt<ST>& C, unsigned long long* stats, uint32_t wave_
     }
 }
 
+// Camera::fuzzy_ray + raytrace's normalize (camera.rs:48-55, raytrace.rs:9) for
+// a fresh stream: draws exactly the two gen_range(0, 1) of block 0 (value0_1 < 1
+// never rejects), so afterwards r is {blk 1, nothing buffered}.
+RT_D V3 camera_dir(const KParams& P, uint32_t px, uint32_t py, Rng& r) {
+    rng_top_up(r);
+    const double fx = (double)px + gen_range(r, 0.0, 1.0);
+    const double fy = (double)py + gen_range(r, 0.0, 1.0);
+    const double x = (2.0 * fx / P.fw - 1.0) * P.tan_x;
+    const double y = -(2.0 * fy / P.fh - 1.0) * P.tan_y;
+    const V3 dir = (load3(P.cam_right) * x + load3(P.cam_up) * y) + load3(P.cam_fwd) * 1.0;
+    return normalize(dir);
+}
+
 // ------------------------------------------------------------ kernels ----
 // path_kernel — persistent waves (one 64-lane wave per workgroup, as many as
 // fit on the chip) pull wave-tiles from a global queue.  A wave-tile is
@@ -1072,6 +1085,7 @@ RT_D void wave_flush(const Cnt<ST>& C, unsigned long long* stats, uint32_t wave_
 // pixel's value — so every pixel is still summed in sample order
 // (main.rs:94-104; bit-identical to the sequential sum when chunks == 1).
 constexpr int kRing = (int)kRingRows;
+constexpr uint32_t kCamSlots = 128;  // precomputed camera rays per wave (two sample rows)
 
 // WAVES = minimum waves per SIMD the register budget must allow (3: 168 VGPRs,
 // 4: 128 VGPRs + spill); RES = the resumable segment form (segment_begin /
@@ -1110,6 +1124,8 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
     __shared__ uint32_t s_n[kShort * kWave];
     __shared__ double s_t[kShort * kWave];
     __shared__ uint32_t s_cnt[kRing];  // finished paths per ring row
+    // camera rays of the next kCamSlots units, [component][slot] (fused kernel only)
+    __shared__ double s_cam[RES ? 1 : 3 * kCamSlots];
     const uint32_t lane = threadIdx.x;
     auto stk = make_stack<RES>(s_n, s_t, 0u, (uint64_t)blockIdx.x * kWave, spill_n, spill_t,
                            gridDim.x * kWave);
@@ -1142,6 +1158,7 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
         __syncthreads();
         V3 sum = v3(0.0, 0.0, 0.0);
         uint32_t base = 0, next = 0, witers = 0;  // wave-uniform schedule
+        uint32_t cam_end = 0;  // camera rays of units [cam_end - kCamSlots, cam_end) are in s_cam
         bool busy = false;
         uint32_t cur = 0, s = 0, b = 0;
         uint64_t pixel = 0;
@@ -1168,6 +1185,26 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
             const uint64_t idle = __ballot(!busy);
             const unsigned long long ph_a = PH_T();
             if (next < limit && idle) {
+                if constexpr (!RES) {
+                    // Camera rays for the units this trip may hand out, one sample row
+                    // (64 units, lane = pixel) at a time with every lane active, instead
+                    // of per path start with only the idle lanes.  Rows
+                    // [cam_end - 128, cam_end - 64) are overwritten only once consumed.
+                    const uint32_t need = min(limit, next + (uint32_t)__popcll(idle));
+                    while (cam_end < need) {
+                        const uint32_t px = qx0 + (lane & 7u), py = qy0 + (lane >> 3);
+                        V3 dir = v3(0.0, 0.0, 0.0);
+                        if (tile_ok && px < P.width && py < P.height) {
+                            Rng cr;
+                            rng_init(cr, P.seed, (uint64_t)py * P.width + px, s0 + cam_end / kWave);
+                            dir = camera_dir(P, px, py, cr);
+                        }
+                        const uint32_t slot = (cam_end + lane) % kCamSlots;
+                        s_cam[slot] = dir.x; s_cam[kCamSlots + slot] = dir.y; s_cam[2 * kCamSlots + slot] = dir.z;
+                        cam_end += kWave;
+                    }
+                    __syncthreads();
+                }
                 const uint32_t k = (uint32_t)__popcll(idle & below);
                 if (!busy && next + k < limit) {
                     cur = next + k;
@@ -1178,14 +1215,14 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
                         // Camera::fuzzy_ray + raytrace (camera.rs:48-55, raytrace.rs:8-10)
                         pixel = (uint64_t)py * P.width + px;
                         rng_init(rng, P.seed, pixel, s);
-                        rng_top_up(rng);
-                        const double fx = (double)px + gen_range(rng, 0.0, 1.0);
-                        const double fy = (double)py + gen_range(rng, 0.0, 1.0);
-                        const double x = (2.0 * fx / P.fw - 1.0) * P.tan_x;
-                        const double y = -(2.0 * fy / P.fh - 1.0) * P.tan_y;
-                        const V3 dir = (load3(P.cam_right) * x + load3(P.cam_up) * y) + load3(P.cam_fwd) * 1.0;
                         ps.o = load3(P.cam_pos);
-                        ps.d = normalize(dir);
+                        if constexpr (!RES) {  // precomputed above: block 0 consumed
+                            const uint32_t slot = cur % kCamSlots;
+                            ps.d = v3(s_cam[slot], s_cam[kCamSlots + slot], s_cam[2 * kCamSlots + slot]);
+                            rng.blk = 1;
+                        } else {
+                            ps.d = camera_dir(P, px, py, rng);
+                        }
                         ps.T = v3(1.0, 1.0, 1.0);
                         ps.L = v3(0.0, 0.0, 0.0);
                         ps.pend = false;
