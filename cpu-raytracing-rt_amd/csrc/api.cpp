@@ -368,6 +368,10 @@ int rt_scene_create(const rt_scene_desc* desc, rt_scene** out) {
         (rc = upload_bvh(s, hs.bvh[2], d.tris)) || (rc = upload_bvh(s, hs.bvh[3], d.lboxes)) ||
         (rc = upload_bvh(s, hs.bvh[4], d.lells)) || (rc = upload_bvh(s, hs.bvh[5], d.ltris)))
         return rc;
+    // ellipsoid reciprocals for dev_quot: computed by the device's own rcp + Newton steps
+    HIP_TRY(launch_ell_rcp(const_cast<DevShape*>(d.ells.shapes), d.ells.n_prims, 0));
+    HIP_TRY(launch_ell_rcp(const_cast<DevShape*>(d.lells.shapes), d.lells.n_prims, 0));
+    HIP_TRY(hipStreamSynchronize(0));
     {  // world normals of plane sides and box faces: rotated(Hit, rot) of render.hip materialise
         std::vector<double> pn(hs.planes.size() * 6), bn(hs.bvh[0].shapes.size() * 24, 0.0);
         for (size_t i = 0; i < hs.planes.size(); ++i) {

@@ -84,6 +84,8 @@ hipError_t launch_unpack_bytes(const double* g, uint8_t* bytes, uint32_t W, uint
                                uint32_t world, uint32_t per_rank, hipStream_t st);
 hipError_t launch_unpack(const double* g, double* img, uint32_t W, uint32_t H, uint32_t tiles_x, uint32_t world,
                          uint32_t per_rank, hipStream_t st);
+// ellipsoid records: aux = dev_rcp(radii), the device's own reciprocals (rt_device.h)
+hipError_t launch_ell_rcp(DevShape* shapes, uint32_t n, hipStream_t st);
 hipError_t launch_fp64_probe(const double* a, const double* b, double* out, uint32_t n, int op, hipStream_t st);
 
 }  // namespace rt

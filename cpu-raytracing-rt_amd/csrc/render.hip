@@ -115,14 +115,14 @@ struct Cand {
 // pos[K] and d[K] bit for bit (finite operands, identity rotation), n.mo =
 // sign * x and n.d = sign * d[K] exactly (the zero terms add signed zeros to a
 // nonzero value), so t = -(sign x) / (sign d[K]) = -RN(x / d[K]) — by
-// fdiv_fast, exact for x in [2^-449, 2^401] (shape_fast).  Returns -1 when the
+// dev_quot, exact for x in [2^-449, 2^401] (shape_fast).  Returns -1 when the
 // lane must take the generic form (x == 0), else hit (1) / miss (0).
 template <int K>
 RT_D int plane_axis_t(const DevShape& s, V3 o, V3 d, const Rcp3& rc, double& t, uint32_t& aux) {
     const double x = comp(o, K) - s.pos[K];
     if (x == 0.0) return -1;
     const double dk = comp(d, K);
-    const double tt = -fdiv_fast(x, dk, comp(rc.r, K));
+    const double tt = -dev_quot(x, dk, comp(rc.r, K));
     if (tt < 0.0) return 0;
     t = tt;
     aux = ((s.axis & 4u) ? -dk : dk) <= 0.0 ? 1u : 0u;
@@ -1451,6 +1451,17 @@ __global__ void unpack_kernel(const double* __restrict__ g, double* __restrict__
     const uint64_t rank = tile % world, slot = tile / world;
     const double* src = g + (((rank * per_rank + slot) * kBlock) + (y % RT_TILE) * RT_TILE + (x % RT_TILE)) * 3;
     img[3 * i] = src[0]; img[3 * i + 1] = src[1]; img[3 * i + 2] = src[2];
+}
+
+__global__ void ell_rcp_kernel(DevShape* __restrict__ s, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    for (int k = 0; k < 3; ++k) s[i].aux[k] = dev_rcp(s[i].shape[k]);
+}
+hipError_t launch_ell_rcp(DevShape* shapes, uint32_t n, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(ell_rcp_kernel, dim3((n + 255) / 256), dim3(256), 0, st, shapes, n);
+    return hipGetLastError();
 }
 
 __global__ void fp64_probe_kernel(const double* a, const double* b, double* out, uint32_t n, int op) {

@@ -185,33 +185,24 @@ struct Cnt {
 };
 
 // ------------------------------------------------------ exact division ----
-// Two exact division forms besides the plain `x / y`:
-//
-// (1) The device's own division, split.  x / y compiles on gfx950 to
-//       d = v_div_scale(y), r = v_rcp(d), two Newton steps r += r * (1 - d*r),
-//       n = v_div_scale(x), q = n*r, rem = fma(-d, q, n),
-//       v_div_fmas(rem, r, q), v_div_fixup
-//     (render.hip ISA).  When neither operand needs div_scale's rescaling,
-//     div_scale returns its operand, div_fmas is fma(rem, r, q) and div_fixup
-//     passes a finite normal quotient through — so the sequence splits into a
-//     per-divisor reciprocal part (dev_rcp: rcp + 4 FMAs) and a per-dividend
-//     quotient part (dev_quot: mul + 2 FMAs) with the SAME bits as x / y.  No
-//     rescaling happens for |y| in [2^-360, 2^360] (dir_ok) and |x| in
-//     [2^-500, 2^402]: the exponent gap stays below 768, the quotient is
-//     normal and the dividend's exponent far above the tiny-numerator case.
-//     A ray's 3 reciprocals then serve every slab and shape quotient of the
-//     ray at 3 ops each (instead of 5 with RN(1/y) below, or ~11 for x / y).
-//     Checked bit for bit against the host's x / y on random and adversarial
-//     pairs of the range (tests/test_gpu_parity.py test_dev_quot_matches_host).
-//
-// (2) fdiv_fast: x / y correctly rounded from r = RN(1/y) (a host constant,
-//     e.g. an ellipsoid's 1/r): q0 = x*r, then two FMA-residual corrections
-//     (Markstein: once q is within 1 ulp, q + (x - q*y)*r rounds to RN(x/y)).
-//     Exact for |x|, |y| in [2^-450, 2^451) (fd_ok: the residuals stay exact);
-//     checked on 1.2e8 adversarial pairs (tools/fastdiv_check.c).
-RT_D bool fd_ok(double v) {
-    return (((uint32_t)((uint64_t)__double_as_longlong(v) >> 52) & 0x7ffu) - 573u) < 901u;
-}
+// The device's own division, split.  x / y compiles on gfx950 to
+//   d = v_div_scale(y), r = v_rcp(d), two Newton steps r += r * (1 - d*r),
+//   n = v_div_scale(x), q = n*r, rem = fma(-d, q, n),
+//   v_div_fmas(rem, r, q), v_div_fixup
+// (render.hip ISA).  When neither operand needs div_scale's rescaling,
+// div_scale returns its operand, div_fmas is fma(rem, r, q) and div_fixup
+// passes a finite normal quotient through — so the sequence splits into a
+// per-divisor reciprocal part (dev_rcp: rcp + 4 FMAs) and a per-dividend
+// quotient part (dev_quot: mul + 2 FMAs) with the SAME bits as x / y.  No
+// rescaling happens for |y| in [2^-360, 2^360] (dir_ok) and |x| in
+// [2^-500, 2^402]: the exponent gap stays below 768, the quotient is
+// normal and the dividend's exponent far above the tiny-numerator case.
+// A ray's 3 reciprocals then serve every slab and shape quotient of the
+// ray at 3 ops each (instead of ~11 for x / y); an ellipsoid's reciprocals
+// are computed once, by the device, into its record.
+// Checked bit for bit against the host's x / y on random and adversarial
+// pairs of the range (tests/test_gpu_parity.py test_dev_quot_matches_host).
+
 // |d| in [2^-360, 2^360]: a ray direction component whose quotients may take dev_quot
 RT_D bool dir_ok(double v) {
     return (((uint32_t)((uint64_t)__double_as_longlong(v) >> 52) & 0x7ffu) - 663u) < 721u;
@@ -233,13 +224,6 @@ RT_D double dev_quot(double x, double y, double r) {
 RT_D double dev_quotz(double x, double y, double r) {
     const double q = dev_quot(x, y, r);
     return x == 0.0 ? x * r : q;
-}
-RT_D double fdiv_fast(double x, double y, double r) {
-    const double q0 = x * r;
-    const double e0 = fma(-q0, y, x);
-    const double q1 = fma(e0, r, q0);
-    const double e1 = fma(-q1, y, x);
-    return fma(e1, r, q1);
 }
 
 // per-axis reciprocals of a ray direction (shared by every slab test of a ray):
@@ -364,7 +348,7 @@ RT_D bool model_ray(const DevShape& s, V3 o, V3 d, V3& mo, V3& md) {
 // without zero components, which rotate_fast returns unchanged (md = d).  Then
 // o, pos and the shape's sizes are 0 or multiples of 2^-449 below 2^401, so
 // every quotient of the box/ellipsoid test has a dividend that is 0 or in
-// [2^-449, 2^402] and takes fdiv_fast(z) exactly.
+// [2^-449, 2^402] and takes dev_quot(z) exactly.
 RT_D bool shape_fast(const DevShape& s, bool rfast, V3 o, V3& mo) {
     if (!rfast || !(s.flags & kShapeFast)) return false;
     mo = o - load3(s.pos);
@@ -426,7 +410,7 @@ RT_D V3 aux_box_normal(uint32_t aux) {
     return v3(0.0, 0.0, s);
 }
 
-// Ellipsoid radii with their host-precomputed reciprocals (DevShape::aux).
+// Ellipsoid radii with their device-computed reciprocals dev_rcp(r) (DevShape::aux).
 struct Radii {
     V3 r, inv;
 };
@@ -436,13 +420,13 @@ RT_D V3 div_radii(V3 v, const Radii& R) {  // v.div_element_wise(r)
 }
 
 // intersect_ellipsoid_coef (ellipsoid.rs:49-76).  FD: shape_fast holds (o
-// and d without zero components, radii fd_ok: o / r and d / r by fdiv_fast)
+// and d without zero components, radii dir_ok: o / r and d / r by dev_quot)
 template <bool FD = false>
 RT_D int ell_coef(const Radii& R, V3 o, V3 d, double& t1o, double& t2o) {
     V3 oo, dd;
     if (FD) {
-        oo = v3(fdiv_fast(o.x, R.r.x, R.inv.x), fdiv_fast(o.y, R.r.y, R.inv.y), fdiv_fast(o.z, R.r.z, R.inv.z));
-        dd = v3(fdiv_fast(d.x, R.r.x, R.inv.x), fdiv_fast(d.y, R.r.y, R.inv.y), fdiv_fast(d.z, R.r.z, R.inv.z));
+        oo = v3(dev_quot(o.x, R.r.x, R.inv.x), dev_quot(o.y, R.r.y, R.inv.y), dev_quot(o.z, R.r.z, R.inv.z));
+        dd = v3(dev_quot(d.x, R.r.x, R.inv.x), dev_quot(d.y, R.r.y, R.inv.y), dev_quot(d.z, R.r.z, R.inv.z));
     } else {
         oo = div_radii(o, R); dd = div_radii(d, R);
     }

@@ -37,12 +37,12 @@ struct alignas(16) DevShape {  // Primitive<T> hot part (scene.rs:20-27)
     double pos[3];
     double rot[4];             // (s, x, y, z)
     // host-precomputed constants (same IEEE ops as the device would do):
-    //   ellipsoid: aux = RN(1/r) per axis (for rt_device.h fdiv_fast)
+    //   ellipsoid: aux = dev_rcp(r) per axis (written by the device, api.cpp)
     //   box:       aux[0] = 1/sum/8 (intersection_probability.rs:15-23)
     double aux[3];
-    // kShapeFast: identity rotation, position (and box sizes / plane normal /
-    // ellipsoid radii) in coord_fast range, nonzero box sizes, fd_ok radii —
-    // a ray_fast ray may then take fdiv_fast for this shape's quotients
+    // kShapeFast: identity rotation, position (and box sizes / plane normal)
+    // in coord_fast range, nonzero box sizes, dir_ok radii — a ray_fast ray
+    // may then take dev_quot for this shape's quotients
     // (rt_device.h shape_fast).  kPlaneAxis: plane normal = sign * e_axis.
     uint32_t flags;
     uint32_t axis;             // plane: 0..2, bit 2 = negative sign

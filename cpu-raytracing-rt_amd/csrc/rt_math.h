@@ -30,7 +30,7 @@ RT_HD V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
 RT_HD V3 operator-(V3 a) { return v3(-a.x, -a.y, -a.z); }
 RT_HD V3 operator*(V3 a, double s) { return v3(a.x * s, a.y * s, a.z * s); }
 RT_HD V3 operator/(V3 a, double s) { return v3(a.x / s, a.y / s, a.z / s); }
-// Coordinate range of the unguarded exact slab division (rt_device.h fdiv_fast):
+// Coordinate range of the unguarded exact slab division (rt_device.h dev_quot):
 // 0, or 2^-397 <= |v| <= 2^400.
 RT_HD bool coord_fast(double v) {
     const double a = v < 0.0 ? -v : v;

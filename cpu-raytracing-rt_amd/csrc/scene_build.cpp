@@ -253,11 +253,11 @@ void flatten(const HostBvh& h, HostBvhArrays& out) {
     out.fast = fast;
 }
 
-// rt_device.h fd_ok on the host: |v| in [2^-450, 2^451)
-static bool fd_ok_host(double v) {
+// rt_device.h dir_ok on the host: |v| in [2^-360, 2^360]
+static bool dir_ok_host(double v) {
     uint64_t b;
     std::memcpy(&b, &v, sizeof b);
-    return ((uint32_t)(b >> 52) & 0x7ffu) - 573u < 901u;
+    return ((uint32_t)(b >> 52) & 0x7ffu) - 663u < 721u;
 }
 // DevShape::flags (rt_layout.h): which shapes a ray_fast ray may test with the
 // unguarded exact division, and planes whose normal is a signed axis
@@ -269,8 +269,8 @@ static uint32_t shape_flags(const rt_shape& s, uint32_t& axis) {
     uint32_t f = 0;
     if (s.type == RT_SHAPE_BOX)
         for (int k = 0; k < 3; ++k) fast = fast && coord_fast(s.shape[k]) && s.shape[k] != 0.0;
-    if (s.type == RT_SHAPE_ELLIPSOID)
-        for (int k = 0; k < 3; ++k) fast = fast && fd_ok_host(s.shape[k]);
+    if (s.type == RT_SHAPE_ELLIPSOID)  // radii in dev_quot's divisor range (rt_device.h dir_ok)
+        for (int k = 0; k < 3; ++k) fast = fast && dir_ok_host(s.shape[k]);
     if (s.type == RT_SHAPE_PLANE) {
         int zeros = 0, k1 = -1;
         for (int k = 0; k < 3; ++k) {
@@ -399,6 +399,7 @@ std::string build_scene(const rt_scene_desc& d, HostScene& out) {
         std::memcpy(it.s.pos, s.position, sizeof(it.s.pos));
         std::memcpy(it.s.rot, s.rotation, sizeof(it.s.rot));
         if (s.type == RT_SHAPE_ELLIPSOID)
+            // placeholder: the device overwrites it with dev_rcp(r) (api.cpp launch_ell_rcp)
             for (int k = 0; k < 3; ++k) it.s.aux[k] = 1.0 / s.shape[k];
         if (s.type == RT_SHAPE_BOX) {
             const double* z = s.shape;
