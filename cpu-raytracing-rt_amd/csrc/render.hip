@@ -801,63 +801,73 @@ RT_D double light_pdf(const DevScene& S, V3 pos, V3 dir, Stk& stk, Cnt<ST>& C) {
 }
 
 // ------------------------------------------------------------ samplers ----
-RT_D V3 uniform_on_sphere(Rng& r) {  // ray_sampler.rs:159-170
-    double a0 = gen_f64(r);
-    rng_top_up(r);  // 6 words here may exceed current + next (see Rng)
-    double a1 = gen_f64(r), a2 = gen_f64(r);
-    return normalize(v3(a0 * 2.0 - 1.0, a1 * 2.0 - 1.0, a2 * 2.0 - 1.0));
+// The diffuse sampler's draws (Mix::sample, ray_sampler.rs:87-93).  After the
+// Mix coin both branches take the same three u64 draws A, B, C of the stream
+// and differ only in how they map them, so the draws (and their Philox
+// refills) run once for the wave instead of once per branch.  The layout
+// (oracle.c diffuse_sample does the same) keeps every distribution:
+//   cosine (ray_sampler.rs:69-76, uniform_on_sphere :159-170): gen_f64 of A, B, C;
+//   box light (uniform_on_box :142-157): choice = gen_range of A, sign = the
+//     lowest bit of A (value0_1 uses only A's top 52 bits, so the two are
+//     independent), u1 / u2 = the inclusive [-1, 1] draws of B / C;
+//   ellipsoid light: uniform_on_sphere of A, B, C; triangle light: u, v of A, B;
+//   the light index (more than one light) is drawn after C.
+RT_D double f64_of(uint64_t u) { return (double)(u >> 11) * (1.0 / 9007199254740992.0); }  // Standard f64
+RT_D double unit_of(uint64_t u) {  // value0_1 (UniformFloat's [0, 1) form)
+    return __longlong_as_double((long long)((u >> 12) | 0x3FF0000000000000ull)) - 1.0;
 }
-RT_D V3 cosine_sample(V3 n, Rng& r) {  // ray_sampler.rs:69-76
-    V3 v = uniform_on_sphere(r);
-    V3 d = v + n;
-    const double eps = kEpsilon * 16.0;
-    if (fabs(d.x) <= eps && fabs(d.y) <= eps && fabs(d.z) <= eps) return n;
-    return normalize(d);
-}
-RT_D double cosine_pdf(V3 n, V3 d) {  // ray_sampler.rs:78-83
-    if (dot(n, d) <= 0.0) return 0.0;
-    return dot(n, d) / kPi;
+RT_D V3 cube_point(uint64_t A, uint64_t B, uint64_t C) {  // uniform_on_sphere before its normalize
+    return v3(f64_of(A) * 2.0 - 1.0, f64_of(B) * 2.0 - 1.0, f64_of(C) * 2.0 - 1.0);
 }
 struct Scales { double s01, s11; };  // new_inclusive scales for [0,1] and [-1,1]
-RT_D V3 uniform_on_box(V3 s, Rng& r, const Scales& sc) {  // ray_sampler.rs:142-157
+RT_D V3 uniform_on_box(V3 s, uint64_t A, uint64_t B, uint64_t C, Rng& r, const Scales& sc) {  // :142-157
     double w4x = s.y * s.z, w4y = s.x * s.z, w4z = s.x * s.y;
-    double choice = gen_range(r, 0.0, (w4x + w4y) + w4z);
-    double sign = (double)(gen_sign_bit(r) * 2 - 1);
-    rng_top_up(r);
-    double u1 = gen_range_incl(r, -1.0, sc.s11);
-    double u2 = gen_range_incl(r, -1.0, sc.s11);
+    const double high = (w4x + w4y) + w4z, scale = high - 0.0;
+    double choice;
+    for (;;) {  // gen_range(0.0, high) (UniformFloat::sample_single): never rejects, kept for form
+        choice = unit_of(A) * scale + 0.0;
+        if (choice < high) break;
+        A = next_u64(r);
+    }
+    const double sign = (A & 1u) ? 1.0 : -1.0;
+    const double u1 = unit_of(B) * sc.s11 + -1.0, u2 = unit_of(C) * sc.s11 + -1.0;  // gen_range(-1.0..=1.0)
     V3 p;
     if (choice < w4x) p = v3(sign, u1, u2);
     else if (choice < w4x + w4y) p = v3(u1, sign, u2);
     else p = v3(u1, u2, sign);
     return mul(p, s);
 }
-RT_D V3 light_point(const DevScene& S, V3 pos, Rng& r, const Scales& sc) {  // ray_sampler.rs:101-129
+RT_D V3 light_point(const DevScene& S, uint64_t A, uint64_t B, uint64_t C, Rng& r,
+                    const Scales& sc) {  // ray_sampler.rs:101-129
     // a one-element range needs no draw (the result is 0 either way; oracle.c gen_range_usize)
     const uint32_t nl = uni_u32(S.n_lights);
-    uint64_t index = nl == 1u ? 0 : gen_index(r, nl, S.light_zone);
-    rng_top_up(r);
+    uint64_t index = 0;
+    if (nl != 1u) {
+        rng_top_up(r);
+        index = gen_index(r, nl, S.light_zone);
+    }
     const uint32_t nb = S.lboxes.n_prims, ne = S.lells.n_prims;
     V3 world;
     if (index < nb) {
         const DevShape l = S.lboxes.shapes[index];
         const Quat q = load_quat(l.rot);
-        world = rotate_fast(q, is_identity(q), uniform_on_box(load3(l.shape), r, sc)) + load3(l.pos);
+        world = rotate_fast(q, is_identity(q), uniform_on_box(load3(l.shape), A, B, C, r, sc)) + load3(l.pos);
     } else if (index < (uint64_t)nb + ne) {
         const DevShape l = S.lells.shapes[index - nb];
         const Quat q = load_quat(l.rot);
-        world = rotate_fast(q, is_identity(q), mul(uniform_on_sphere(r), load3(l.shape))) + load3(l.pos);
+        world = rotate_fast(q, is_identity(q), mul(normalize(cube_point(A, B, C)), load3(l.shape))) + load3(l.pos);
     } else {
         const DevTri t = S.ltris.tris[index - nb - ne];
-        double u = gen_range_incl(r, 0.0, sc.s01);
-        double v = gen_range_incl(r, 0.0, sc.s01);
+        double u = unit_of(A) * sc.s01 + 0.0;  // gen_range(0.0..=1.0)
+        double v = unit_of(B) * sc.s01 + 0.0;
         if (u + v > 1.0) { u = 1.0 - u; v = 1.0 - v; }
         world = (load3(t.ba) * u + load3(t.ca) * v) + load3(t.a);
     }
     return world;
 }
-RT_D V3 light_sample(const DevScene& S, V3 pos, Rng& r, const Scales& sc) {  // ray_sampler.rs:101-130
-    return normalize(light_point(S, pos, r, sc) - pos);
+RT_D double cosine_pdf(V3 n, V3 d) {  // ray_sampler.rs:78-83
+    if (dot(n, d) <= 0.0) return 0.0;
+    return dot(n, d) / kPi;
 }
 
 // --------------------------------------------------------- integrator ----
@@ -932,17 +942,21 @@ RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, P
         const bool empty = S.n_lights == 0;
         V3 dir;
         const bool by_cosine = empty || gen_half(rng);  // Mix::sample (ray_sampler.rs:87-93)
+        // the draws both samplers share (see "samplers"); the words are in the current
+        // block and the next one (after the coin) or the next two (no coin)
+        const uint64_t ua = next_u64(rng);
         rng_top_up(rng);
+        const uint64_t ub = next_u64(rng), uc = next_u64(rng);
         // both samplers end in normalize(w): one call after the branches join
         V3 sw;
         bool degen = false;
         if (by_cosine) {
-            sw = uniform_on_sphere(rng) + h.ns;  // cosine_sample (ray_sampler.rs:69-76)
+            sw = normalize(cube_point(ua, ub, uc)) + h.ns;  // cosine_sample (ray_sampler.rs:69-76)
             const double eps = kEpsilon * 16.0;
             degen = fabs(sw.x) <= eps && fabs(sw.y) <= eps && fabs(sw.z) <= eps;
         } else {
             const unsigned long long ph1 = PH_T();
-            sw = light_point(S, pos, rng, sc) - pos;
+            sw = light_point(S, ua, ub, uc, rng, sc) - pos;
             PH_ADDW(kPhLightSample, ph1);
         }
         dir = degen ? h.ns : normalize(sw);

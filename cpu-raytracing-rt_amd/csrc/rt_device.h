@@ -154,9 +154,6 @@ RT_D uint64_t gen_index(Rng& r, uint64_t range, uint64_t zone) {
         if (lo <= zone) return hi;
     }
 }
-// UniformInt<i32>::sample_single_inclusive(0, 1) with the exact zone (oracle.c
-// gen_range_i32_0_1): range 2 never rejects, the result is the word's top bit
-RT_D int32_t gen_sign_bit(Rng& r) { return (int32_t)(next_u32(r) >> 31); }
 // Bernoulli(0.5) from one word: P(w < 2^31) = 1/2 exactly (oracle.c gen_half)
 RT_D bool gen_half(Rng& r) { return next_u32(r) < 0x80000000u; }
 RT_D bool gen_bool(Rng& r, double p) {  // Bernoulli

@@ -791,16 +791,6 @@ static uint64_t gen_range_usize(Rng* r, uint64_t n) { /* UniformInt<usize>::samp
         if (lo <= zone) return hi;
     }
 }
-static int32_t gen_range_i32_0_1(Rng* r) { /* UniformInt<i32>::sample_single_inclusive(0, 1) */
-    const uint32_t range = 2;
-    const uint32_t zone = UINT32_MAX - (0u - range) % range; /* exact zone (see usize_zone): no rejection */
-    for (;;) {
-        uint32_t v = next_u32(r);
-        uint64_t m = (uint64_t)v * range;
-        uint32_t hi = (uint32_t)(m >> 32), lo = (uint32_t)m;
-        if (lo <= zone) return (int32_t)hi;
-    }
-}
 /* Bernoulli(0.5) from ONE word: P(w < 2^31) = 1/2 exactly, the distribution of
    gen_bool(0.5) (whose u64 draw this stream layout does not spend).  With one
    word for the Mix coin (and none for a single light's index), every diffuse
@@ -815,34 +805,55 @@ static int gen_bool(Rng* r, double p) { /* Bernoulli::new(p) + sample */
 /* ======================================================================= */
 /* ray_sampler.rs                                                           */
 /* ======================================================================= */
-static V3 uniform_on_sphere(Rng* r) { /* :159-170 (a normalised cube point) */
-    double a0 = gen_f64(r), a1 = gen_f64(r), a2 = gen_f64(r);
-    return vnormalize(v3(a0 * 2.0 - 1.0, a1 * 2.0 - 1.0, a2 * 2.0 - 1.0));
+/* The diffuse sampler's stream layout (Mix::sample :87-93): after the Mix coin both
+   branches take the same three u64 draws A, B, C and differ only in how they map them
+   (the device then draws them once per wave, render.hip "samplers").  Every
+   distribution is the reference's:
+     cosine (:69-76, uniform_on_sphere :159-170): gen_f64 of A, B, C;
+     box light (uniform_on_box :142-157): choice = gen_range of A, sign = the lowest bit
+       of A (value0_1 reads only A's top 52 bits, so the two are independent), u1 / u2
+       = the inclusive [-1, 1] draws of B / C;
+     ellipsoid light: uniform_on_sphere of A, B, C; triangle light: u, v of A, B;
+     the light index (more than one light) is drawn after C. */
+static inline double f64_of(uint64_t u) { return (double)(u >> 11) * (1.0 / 9007199254740992.0); }
+static inline double unit_of(uint64_t u) { return bits_f64((u >> 12) | 0x3FF0000000000000ull) - 1.0; }
+static V3 sphere_of(uint64_t A, uint64_t B, uint64_t C) { /* uniform_on_sphere :159-170 (a normalised cube point) */
+    return vnormalize(v3(f64_of(A) * 2.0 - 1.0, f64_of(B) * 2.0 - 1.0, f64_of(C) * 2.0 - 1.0));
 }
-static V3 cosine_sample(V3 n, Rng* r) { /* :69-76 */
-    V3 v = uniform_on_sphere(r);
+static V3 uniform_on_sphere(Rng* r) {
+    uint64_t A = next_u64(r), B = next_u64(r), C = next_u64(r);
+    return sphere_of(A, B, C);
+}
+static V3 cosine_of(V3 n, V3 v) { /* :69-76 with v = uniform_on_sphere */
     V3 d = vadd(v, n);
     const double eps = R_EPSILON * 16.0;
     if (fabs(d.x) <= eps && fabs(d.y) <= eps && fabs(d.z) <= eps) return n; /* abs_diff_eq(zero) */
     return vnormalize(d);
 }
+static V3 cosine_sample(V3 n, Rng* r) { return cosine_of(n, uniform_on_sphere(r)); } /* :69-76 */
 static inline double cosine_pdf(V3 n, V3 d) { /* :78-83 */
     if (vdot(n, d) <= 0.0) return 0.0;
     return vdot(n, d) / R_PI;
 }
-static V3 uniform_on_box(V3 s, Rng* r) { /* :142-157 */
+static V3 uniform_on_box(V3 s, uint64_t A, uint64_t B, uint64_t C, Rng* r) { /* :142-157 */
     double w4x = s.y * s.z, w4y = s.x * s.z, w4z = s.x * s.y;
-    double choice = gen_range_f64(r, 0.0, (w4x + w4y) + w4z);
-    double sign = (double)(gen_range_i32_0_1(r) * 2 - 1);
-    double u1 = gen_range_incl_f64(r, -1.0, 1.0);
-    double u2 = gen_range_incl_f64(r, -1.0, 1.0);
+    double high = (w4x + w4y) + w4z, scale = high - 0.0, choice;
+    for (;;) { /* gen_range_f64(r, 0.0, high) on A (never rejects: value0_1 * scale < scale) */
+        choice = unit_of(A) * scale + 0.0;
+        if (choice < high) break;
+        A = next_u64(r);
+    }
+    double sign = (A & 1u) ? 1.0 : -1.0;
+    double s11 = incl_scale(-1.0, 1.0);
+    double u1 = unit_of(B) * s11 + -1.0; /* gen_range_incl_f64(-1.0, 1.0) */
+    double u2 = unit_of(C) * s11 + -1.0;
     V3 p;
     if (choice < w4x) p = v3(sign, u1, u2);
     else if (choice < w4x + w4y) p = v3(u1, sign, u2);
     else p = v3(u1, u2, sign);
     return vmul(p, s);
 }
-static V3 light_sample(const oracle_scene* s, V3 pos, Rng* r) { /* :101-130 */
+static V3 light_sample(const oracle_scene* s, V3 pos, uint64_t A, uint64_t B, uint64_t C, Rng* r) { /* :101-130 */
     uint64_t len = s->lells.n + s->lboxes.n + s->ltris.n;
     /* gen_range(0..1) is 0 whatever it draws: no draw for a single light (a choice of
        this build's stream layout, like rng_align; the distribution is the same) */
@@ -850,14 +861,15 @@ static V3 light_sample(const oracle_scene* s, V3 pos, Rng* r) { /* :101-130 */
     V3 world;
     if (index < s->lboxes.n) {
         const Shape* l = &s->lboxes.s[index];
-        world = vadd(qrot(l->rot, uniform_on_box(l->shape, r)), l->pos);
+        world = vadd(qrot(l->rot, uniform_on_box(l->shape, A, B, C, r)), l->pos);
     } else if (index < s->lboxes.n + s->lells.n) {
         const Shape* l = &s->lells.s[index - s->lboxes.n];
-        world = vadd(qrot(l->rot, vmul(uniform_on_sphere(r), l->shape)), l->pos);
+        world = vadd(qrot(l->rot, vmul(sphere_of(A, B, C), l->shape)), l->pos);
     } else {
         const Triangle* t = &s->ltris.t[index - s->lboxes.n - s->lells.n].tri;
-        double u = gen_range_incl_f64(r, 0.0, 1.0);
-        double v = gen_range_incl_f64(r, 0.0, 1.0);
+        double s01 = incl_scale(0.0, 1.0);
+        double u = unit_of(A) * s01 + 0.0; /* gen_range_incl_f64(0.0, 1.0) */
+        double v = unit_of(B) * s01 + 0.0;
         if (u + v > 1.0) { u = 1.0 - u; v = 1.0 - v; }
         world = vadd(vadd(vscale(t->ba, u), vscale(t->ca, v)), t->a);
     }
@@ -908,7 +920,11 @@ static int diffuse_sample(Ctx* x, V3 pos, V3 n, V3* dir_out, double* pdf_out) {
     V3 dir;
     int empty = lights_empty(s);
     if (empty) dir = cosine_sample(n, x->rng);
-    else dir = gen_half(x->rng) ? cosine_sample(n, x->rng) : light_sample(s, pos, x->rng); /* Mix::sample :87-93 */
+    else { /* Mix::sample :87-93, with the shared draws A, B, C (see uniform_on_box) */
+        int coin = gen_half(x->rng);
+        uint64_t A = next_u64(x->rng), B = next_u64(x->rng), C = next_u64(x->rng);
+        dir = coin ? cosine_of(n, sphere_of(A, B, C)) : light_sample(s, pos, A, B, C, x->rng);
+    }
     if (vdot(dir, n) <= 0.0) return 0;
     double pdf = empty ? cosine_pdf(n, dir)
                        : (cosine_pdf(n, dir) + light_pdf(s, pos, dir, x->c)) / 2.0; /* Mix::pdf :95-97 */
@@ -1182,7 +1198,8 @@ void oracle_sampler_draws(uint64_t seed, uint64_t pixel, uint32_t sample, int ki
         V3 v = v3(0, 0, 0);
         switch (kind) {
         case 0: v = cosine_sample(vld(arg), &r); break;
-        case 1: v = uniform_on_box(vld(arg), &r); break;
+        case 1: { uint64_t A = next_u64(&r), B = next_u64(&r), C = next_u64(&r);
+                  v = uniform_on_box(vld(arg), A, B, C, &r); } break;
         case 2: v = uniform_on_sphere(&r); break;
         case 3: v.x = (double)gen_range_usize(&r, (uint64_t)arg[0]); break;
         case 4: v.x = (double)gen_bool(&r, arg[0]); break;

@@ -142,6 +142,12 @@ def test_samplers_geometry(orc):
     face = np.argmax(np.isclose(np.abs(pts) / s, 1.0, rtol=0, atol=1e-15), axis=1)
     w = np.array([s[1] * s[2], s[0] * s[2], s[0] * s[1]])
     np.testing.assert_allclose(np.bincount(face, minlength=3) / len(face), w / w.sum(), atol=0.03)
+    # the face's sign (the lowest bit of the choice draw): +-1 equally likely on each face
+    sign = np.sign(pts[np.arange(len(pts)), face])
+    assert set(np.unique(sign)) == {-1.0, 1.0}
+    for f in range(3):
+        on = sign[face == f]
+        assert abs(on.mean()) < 4.0 / np.sqrt(max(len(on), 1)) + 1e-9, (f, len(on), on.mean())
     sph = orc.sampler_draws(7, 1, 0, 2, [0, 0, 0], 2000)
     np.testing.assert_allclose(np.linalg.norm(sph, axis=1), 1.0, atol=1e-15)
     n = np.array([0.0, 1.0, 0.0])
