@@ -941,12 +941,11 @@ RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, P
         V3 pos = o + d * h.t;
         const bool empty = S.n_lights == 0;
         V3 dir;
-        const bool by_cosine = empty || gen_half(rng);  // Mix::sample (ray_sampler.rs:87-93)
-        // the draws both samplers share (see "samplers"); the words are in the current
-        // block and the next one (after the coin) or the next two (no coin)
-        const uint64_t ua = next_u64(rng);
-        rng_top_up(rng);
-        const uint64_t ub = next_u64(rng), uc = next_u64(rng);
+        // Mix::sample (ray_sampler.rs:87-93): the coin (when there are lights), then the
+        // three draws both samplers share (see "samplers")
+        bool by_cosine;
+        uint64_t ua, ub, uc;
+        diffuse_draws(rng, !empty, by_cosine, ua, ub, uc);
         // both samplers end in normalize(w): one call after the branches join
         V3 sw;
         bool degen = false;

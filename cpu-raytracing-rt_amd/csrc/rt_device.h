@@ -121,6 +121,36 @@ RT_D uint64_t next_u64(Rng& r) {
     uint64_t hi = next_u32(r);
     return lo | (hi << 32);
 }
+// The draws of a diffuse shading step (render.hip segment_shade: the Mix coin
+// word when `coin_draw`, then three u64) read straight from the block words.
+// Precondition: rng_align + rng_top_up just ran, so nothing is buffered and the
+// next block b sits in n0/n1 (nready) — true at every hit.  The words are those
+// next_u32 / next_u64 would return (block b, then block b + 1, generated here
+// as rng_top_up would), and the state afterwards is theirs too, without the
+// per-word queue bookkeeping.
+RT_D void diffuse_draws(Rng& r, bool coin_draw, bool& coin, uint64_t& A, uint64_t& B, uint64_t& C) {
+    const uint64_t b0 = r.n0, b1 = r.n1;  // w0 | w1 << 32, w2 | w3 << 32 of block b
+    uint64_t m0, m1;                      // block b + 1
+    PH_COUNT(kPhRngWave, kPhRngLane);
+    philox(r.blk, r.sample, r.pix_lo, r.pix_hi, r.k0, r.k1, m0, m1);
+    r.blk++;
+    r.nready = 0;
+    r.q1 = 0;
+    if (coin_draw) {
+        coin = (uint32_t)b0 < 0x80000000u;  // gen_half: word w0
+        A = (b0 >> 32) | (b1 << 32);        // w1, w2
+        B = (b1 >> 32) | (m0 << 32);        // w3, block b + 1 w0
+        C = (m0 >> 32) | (m1 << 32);        // w1, w2 of block b + 1
+        r.q0 = m1 >> 32;                    // w3 of block b + 1 left
+        r.avail = 1;
+    } else {
+        coin = true;
+        A = b0; B = b1; C = m0;
+        r.q0 = m1;
+        r.avail = 2;
+    }
+}
+
 // rand 0.8.5 transforms (see oracle.c header for the full list)
 RT_D double gen_f64(Rng& r) { return (double)(next_u64(r) >> 11) * (1.0 / 9007199254740992.0); }
 RT_D double value0_1(Rng& r) {
