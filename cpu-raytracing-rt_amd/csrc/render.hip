@@ -629,7 +629,12 @@ template <bool ST>
 RT_D bool intersect_tail(const DevScene& S, const Cand& best, V3 o, V3 d, Cnt<ST>& C, Hit& out, uint32_t& mat,
                          int32_t& gid) {
     if (!best.valid) return false;
-    if (!(best.t * magnitude(d) <= INFINITY)) return false;  // :56
+    // :56, t * d.magnitude() <= +inf, i.e. the product is not NaN.  With dd = d.d
+    // (>= 0 or NaN), sqrt(dd) is NaN / 0 / inf exactly when dd is, so the product
+    // is NaN iff t or dd is NaN, or t is inf and dd 0, or t is 0 and dd inf: the
+    // same outcome without the square root.
+    const double dd = dot(d, d);
+    if (isnan(best.t) || isnan(dd) || (isinf(best.t) && dd == 0.0) || (best.t == 0.0 && isinf(dd))) return false;
     const unsigned long long ph = PH_T();
     Quat rot;
     bool world;
