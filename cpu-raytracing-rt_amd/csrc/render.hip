@@ -129,6 +129,24 @@ RT_D int plane_axis_t(const DevShape& s, V3 o, V3 d, const Rcp3& rc, double& t, 
     return 1;
 }
 
+// box_coef on a generic model-space ray (model_ray; `same`: md == d, whose
+// reciprocals rc may serve).  For a kBoxSizes box the dividends +-s - mo are 0
+// or in dev_quot's range whenever |mo| <= 2^400 (s and mo are then both 0 or
+// at least 2^-420 apart from tiny cases that leave s - mo near s), so when md
+// also has every component dir_ok in every lane running this, the wave takes
+// the split division (box_coef<true>, with md's own dev_rcp reciprocals): the
+// same bits as the quotients of the plain form.
+RT_D int box_model(const DevShape& s, V3 mo, V3 md, bool same, const Rcp3& rc, Bpi& en, Bpi& ex) {
+#ifndef RT_NO_FASTSHAPE
+    if (s.flags & kBoxSizes) {
+        const bool ok = dir_ok(md.x) && dir_ok(md.y) && dir_ok(md.z) && fabs(mo.x) <= 0x1p400 &&
+                        fabs(mo.y) <= 0x1p400 && fabs(mo.z) <= 0x1p400;
+        if (__ballot(!ok) == 0) return box_coef<true>(load3(s.shape), mo, md, same ? rc : make_rcp3(md), en, ex);
+    }
+#endif
+    return box_coef(load3(s.shape), mo, md, rc, en, ex);
+}
+
 // closest hit of one shape in model space; t + aux.  rfast: the ray passed
 // ray_fast (kShapeFast shapes may then take the exact unguarded division).
 template <int KIND>
@@ -160,7 +178,7 @@ RT_D bool shape_closest(const DevShape& s, V3 o, V3 d, const Rcp3& rc, bool rfas
     if (KIND == 0) return plane_t(load3(s.shape), mo, md, t, aux);
     if (KIND == 1) {
         Bpi en, ex;
-        int k = box_coef(load3(s.shape), mo, md, same ? rc : make_rcp3(md), en, ex);
+        int k = box_model(s, mo, md, same, rc, en, ex);
         if (k == 2) { t = en.t; aux = bpi_aux(en, false); return true; }
         if (k == 1) { t = ex.t; aux = bpi_aux(ex, true); return true; }
         return false;
@@ -498,7 +516,7 @@ RT_D int box_test(const DevShape& s, V3 o, V3 d, const Rcp3& rc, bool rfast, Bpi
     if (shape_fast(s, rfast, o, mo)) return box_coef<true>(load3(s.shape), mo, d, rc, en, ex);
 #endif
     const bool same = model_ray(s, o, d, mo, md);
-    return box_coef(load3(s.shape), mo, md, same ? rc : make_rcp3(md), en, ex);
+    return box_model(s, mo, md, same, rc, en, ex);
 }
 // The Light::pdf callback terms of one light box crossing (leaf_all<1>:
 // intersection_probability.rs:15-23, ray_sampler.rs:132-139,172-174)
@@ -711,8 +729,7 @@ RT_D void leaf_all(const DevBvh& B, uint32_t start, uint32_t cnt, V3 o, V3 d, co
             V3 sz = load3(s.shape);
             if (KIND == 1) {
                 Bpi en, ex;
-                int k = fs ? box_coef<true>(sz, mo, md, rc, en, ex)
-                           : box_coef(sz, mo, md, same ? rc : make_rcp3(md), en, ex);
+                int k = fs ? box_coef<true>(sz, mo, md, rc, en, ex) : box_model(s, mo, md, same, rc, en, ex);
                 const double pb = s.aux[0];
                 // |d . normalize(rotate(q, n))| for a face normal n = sign * e_dim.  With an
                 // identity q, rotate returns n up to the signs of its zero components and

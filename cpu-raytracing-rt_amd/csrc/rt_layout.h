@@ -47,7 +47,9 @@ struct alignas(16) DevShape {  // Primitive<T> hot part (scene.rs:20-27)
     uint32_t flags;
     uint32_t axis;             // plane: 0..2, bit 2 = negative sign
 };
-constexpr uint32_t kShapeFast = 1u, kPlaneAxis = 2u;
+// kBoxSizes: a box whose half sizes are nonzero and in coord_fast range (any
+// rotation): box_model may then take dev_quot on the model-space ray.
+constexpr uint32_t kShapeFast = 1u, kPlaneAxis = 2u, kBoxSizes = 4u;
 static_assert(sizeof(DevShape) == 112, "shape record");
 
 struct alignas(16) DevTri {    // Triangle hot part (triangle.rs:5-17)

@@ -267,8 +267,12 @@ static uint32_t shape_flags(const rt_shape& s, uint32_t& axis) {
     bool fast = q[0] == 1.0 && q[1] == 0.0 && q[2] == 0.0 && q[3] == 0.0;
     for (int k = 0; k < 3; ++k) fast = fast && coord_fast(s.position[k]);
     uint32_t f = 0;
-    if (s.type == RT_SHAPE_BOX)
-        for (int k = 0; k < 3; ++k) fast = fast && coord_fast(s.shape[k]) && s.shape[k] != 0.0;
+    if (s.type == RT_SHAPE_BOX) {
+        bool sizes = true;
+        for (int k = 0; k < 3; ++k) sizes = sizes && coord_fast(s.shape[k]) && s.shape[k] != 0.0;
+        fast = fast && sizes;
+        if (sizes) f |= kBoxSizes;
+    }
     if (s.type == RT_SHAPE_ELLIPSOID)  // radii in dev_quot's divisor range (rt_device.h dir_ok)
         for (int k = 0; k < 3; ++k) fast = fast && dir_ok_host(s.shape[k]);
     if (s.type == RT_SHAPE_PLANE) {

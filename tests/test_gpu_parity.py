@@ -447,6 +447,63 @@ IOR 1.5
 """
 
 
+ROTBOX_SCENE = """DIMENSIONS 20 16
+SAMPLES 3
+RAY_DEPTH 8
+BG_COLOR 0.1 0.1 0.1
+CAMERA_POSITION 0 0 -2
+NEW_PRIMITIVE
+PLANE 0 1 0
+POSITION 0 -1 0
+COLOR 0.7 0.7 0.7
+NEW_PRIMITIVE
+BOX 0.25 0.5 0.25
+POSITION 0.25 -0.5 0.5
+ROTATION 0 0.7071067811865476 0 0.7071067811865476
+COLOR 0.8 0.8 0.8
+NEW_PRIMITIVE
+BOX 0.3 0.1 0.2
+POSITION -0.5 0.25 0
+ROTATION 0.2 0.3 0.1 0.9273618495495704
+EMISSION 4 4 4
+NEW_PRIMITIVE
+BOX 0.125 0.25 0.5
+POSITION 0 0.5 0.25
+ROTATION 0 0 0.3826834323650898 0.9238795325112867
+COLOR 0.5 0.6 0.7
+METALLIC
+"""
+
+
+def test_rotated_box_edges(rt, orc):
+    """Rotated boxes take the split division on their model-space ray when every lane
+    of the wave has md dir_ok and |mo| <= 2^400 (render.hip box_model), the plain
+    quotients otherwise.  Axis and diagonal directions give zero md components (the
+    plain form), dyadic origins exact zeros in mo; hits, light sums and pdfs must equal
+    the oracle's bit for bit."""
+    desc, params = rt.parse_scene(ROTBOX_SCENE)
+    g, o = rt.Scene(desc), orc.OracleScene(desc)
+    rng = np.random.default_rng(5)
+    n = 40000
+    orig = rng.integers(-8, 9, (n, 3)) / 8.0
+    orig[n // 2:] += rng.uniform(-1e-3, 1e-3, (n - n // 2, 3))
+    d = rng.standard_normal((n, 3))
+    d[:4000] = rng.integers(-2, 3, (4000, 3)) / 2.0
+    d[:4000][np.all(d[:4000] == 0, axis=1)] = [1.0, 0.0, 0.0]
+    rays = np.concatenate([orig, d], axis=1)
+    gh, oh = g.intersect(rays), o.intersect(rays)
+    assert np.array_equal(gh.view(np.uint8), oh.view(np.uint8))
+    assert (gh["prim"] >= 1).sum() > n // 10  # boxes hit
+    gi, gc = g.intersect_lights(rays)
+    oi, oc = o.intersect_lights(rays)
+    assert np.array_equal(gc, oc) and gc.sum() > 1000
+    assert np.array_equal(gi.view(np.uint64), oi.view(np.uint64))
+    dn = d / np.linalg.norm(d, axis=1, keepdims=True)
+    pd = np.concatenate([orig, dn], axis=1)
+    assert np.array_equal(g.light_pdf(pd).view(np.uint64), o.light_pdf(pd).view(np.uint64))
+    _compare(g, o, params)
+
+
 def test_fast_shape_edges(rt, orc):
     """Identity-rotation shapes and signed-axis planes take the exact unguarded
     division for ray_fast rays (rt_device.h shape_fast, plane_axis_t).  Dyadic
