@@ -657,17 +657,19 @@ int rt_bvh_build(const double* boxes, uint64_t n, uint64_t* n_nodes, int64_t* ou
     return RT_OK;
 }
 
-// Diagnostic: device f64 sqrt (op 0), division (op 1) and the split division
-// dev_quot(a, b, dev_rcp(b)) (op 2) for bit-exactness checks.
+// Diagnostic: device f64 sqrt (op 0), division (op 1), the split division
+// dev_quot(a, b, dev_rcp(b)) (op 2), dev_sqrt(a) (op 3) and dev_inv_len(a)
+// (op 4) for bit-exactness checks.
 int rt_probe_fp64(int op, const double* a, const double* b, uint32_t n, double* out) {
-    if (!a || !out || (op >= 1 && !b) || op < 0 || op > 2) return set_error(RT_ERR_INVALID, "bad arguments");
+    const bool two = op == 1 || op == 2;
+    if (!a || !out || (two && !b) || op < 0 || op > 4) return set_error(RT_ERR_INVALID, "bad arguments");
     if (n == 0) return RT_OK;
     DevBuf<double> da, db, dout;
     HIP_TRY(da.alloc(n));
     HIP_TRY(db.alloc(n));
     HIP_TRY(dout.alloc(n));
     HIP_TRY(hipMemcpy(da.p, a, n * sizeof(double), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(db.p, op >= 1 ? b : a, n * sizeof(double), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(db.p, two ? b : a, n * sizeof(double), hipMemcpyHostToDevice));
     HIP_TRY(launch_fp64_probe(da.p, db.p, dout.p, n, op, 0));
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(out, dout.p, n * sizeof(double), hipMemcpyDeviceToHost));

@@ -461,7 +461,7 @@ RT_D Hit materialise(const DevScene& S, const Cand& c, V3 o, V3 d, Quat& rot, ui
         const DevBvh& B = S.tris;
         const DevTriCold& tc = B.tri_cold[c.prim];
         V3 n = load3(tc.ng), na = load3(tc.na), nb = load3(tc.nb), nc = load3(tc.nc);
-        V3 sn = normalize(na + (nb - na) * c.u + (nc - na) * c.v);
+        V3 sn = nrm(na + (nb - na) * c.u + (nc - na) * c.v);
         bool inside = dot(d, n) > 0.0;
         h.ng = inside ? -n : n;
         h.ns = inside ? -sn : sn;
@@ -500,7 +500,7 @@ RT_D Hit materialise(const DevScene& S, const Cand& c, V3 o, V3 d, Quat& rot, ui
         if (inside) n = -n;
         // both normals are this n, so with_rotated_normal's two rotate + normalize
         // results are the same bits: computed once here (world = true)
-        n = normalize(rotate_fast(rot, is_identity(rot), n));
+        n = nrm(rotate_fast(rot, is_identity(rot), n));
         h.ng = n; h.ns = n; h.inside = inside;
         world = true;
     }
@@ -527,12 +527,12 @@ RT_D void box_light_terms(const DevShape& s, int k, const Bpi& en, const Bpi& ex
     const Quat q = load_quat(s.rot);
     const bool qid = is_identity(q);
     if (k == 2) {
-        const double dn = qid ? fabs(comp(d, en.dim)) : fabs(dot(d, normalize(rotate(q, bpi_normal(en)))));
+        const double dn = qid ? fabs(comp(d, en.dim)) : fabs(dot(d, nrm(rotate(q, bpi_normal(en)))));
         impact += pb * (en.t * en.t / dn);
         C.lhit();
     }
     if (k >= 1) {
-        const double dn = qid ? fabs(comp(d, ex.dim)) : fabs(dot(d, normalize(rotate(q, bpi_normal(ex)))));
+        const double dn = qid ? fabs(comp(d, ex.dim)) : fabs(dot(d, nrm(rotate(q, bpi_normal(ex)))));
         impact += pb * (ex.t * ex.t / dn);
         C.lhit();
     }
@@ -736,12 +736,12 @@ RT_D void leaf_all(const DevBvh& B, uint32_t start, uint32_t cnt, V3 o, V3 d, co
                 // normalize leaves a unit axis vector unchanged, so the dot is +-d[dim] up to
                 // signed zeros, which fabs discards: exactly |d[dim]|.
                 if (k == 2) {
-                    const double dn = qid ? fabs(comp(d, en.dim)) : fabs(dot(d, normalize(rotate(q, bpi_normal(en)))));
+                    const double dn = qid ? fabs(comp(d, en.dim)) : fabs(dot(d, nrm(rotate(q, bpi_normal(en)))));
                     impact += pb * (en.t * en.t / dn);
                     C.lhit(); nhits++;
                 }
                 if (k >= 1) {
-                    const double dn = qid ? fabs(comp(d, ex.dim)) : fabs(dot(d, normalize(rotate(q, bpi_normal(ex)))));
+                    const double dn = qid ? fabs(comp(d, ex.dim)) : fabs(dot(d, nrm(rotate(q, bpi_normal(ex)))));
                     impact += pb * (ex.t * ex.t / dn);
                     C.lhit(); nhits++;
                 }
@@ -750,12 +750,12 @@ RT_D void leaf_all(const DevBvh& B, uint32_t start, uint32_t cnt, V3 o, V3 d, co
                 const Radii R = load_radii(s);
                 int k = fs ? ell_coef<true>(R, mo, md, t1, t2) : ell_coef(R, mo, md, t1, t2);
                 if (k == 2) {
-                    V3 ng = normalize(rotate_fast(q, qid, ell_normal(R, mo, md, t1)));
+                    V3 ng = nrm(rotate_fast(q, qid, ell_normal(R, mo, md, t1)));
                     impact += prob_ell(sz, ng) * (t1 * t1 / fabs(dot(d, ng)));
                     C.lhit(); nhits++;
                 }
                 if (k >= 1) {
-                    V3 ng = normalize(rotate_fast(q, qid, -ell_normal(R, mo, md, t2)));
+                    V3 ng = nrm(rotate_fast(q, qid, -ell_normal(R, mo, md, t2)));
                     impact += prob_ell(sz, ng) * (t2 * t2 / fabs(dot(d, ng)));
                     C.lhit(); nhits++;
                 }
@@ -877,7 +877,7 @@ RT_D V3 light_point(const DevScene& S, uint64_t A, uint64_t B, uint64_t C, Rng& 
     } else if (index < (uint64_t)nb + ne) {
         const DevShape l = S.lells.shapes[index - nb];
         const Quat q = load_quat(l.rot);
-        world = rotate_fast(q, is_identity(q), mul(normalize(cube_point(A, B, C)), load3(l.shape))) + load3(l.pos);
+        world = rotate_fast(q, is_identity(q), mul(nrm(cube_point(A, B, C)), load3(l.shape))) + load3(l.pos);
     } else {
         const DevTri t = S.ltris.tris[index - nb - ne];
         double u = unit_of(A) * sc.s01 + 0.0;  // gen_range(0.0..=1.0)
@@ -972,7 +972,7 @@ RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, P
         V3 sw;
         bool degen = false;
         if (by_cosine) {
-            sw = normalize(cube_point(ua, ub, uc)) + h.ns;  // cosine_sample (ray_sampler.rs:69-76)
+            sw = nrm(cube_point(ua, ub, uc)) + h.ns;  // cosine_sample (ray_sampler.rs:69-76)
             const double eps = kEpsilon * 16.0;
             degen = fabs(sw.x) <= eps && fabs(sw.y) <= eps && fabs(sw.z) <= eps;
         } else {
@@ -980,7 +980,7 @@ RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, P
             sw = light_point(S, ua, ub, uc, rng, sc) - pos;
             PH_ADDW(kPhLightSample, ph1);
         }
-        dir = degen ? h.ns : normalize(sw);
+        dir = degen ? h.ns : nrm(sw);
         const double cs = dot(dir, h.ns);
         if (cs <= 0.0) return false;
         if (SLT && more && uni_u32(S.slt_mask)) {
@@ -1017,7 +1017,7 @@ RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, P
         const double k = h.inside ? m.ior : m.k_out;
         // refracted_ray (raytrace.rs:75-88)
         const double cos1 = -dot(h.ns, d);
-        const double sin2 = k * sqrt(1.0 - cos1 * cos1);
+        const double sin2 = k * dev_sqrt(1.0 - cos1 * cos1);
         bool reflect = true;
         if (!(sin2 > 1.0)) {
             const double r0 = m.r0;  // ((n1 - n2) / (n1 + n2)).powi(2)
@@ -1027,7 +1027,7 @@ RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, P
             if (p > 1.0) p = 1.0;
             reflect = gen_bool(rng, p);
             if (!reflect) {
-                const double cos2 = sqrt(1.0 - sin2 * sin2);
+                const double cos2 = dev_sqrt(1.0 - sin2 * sin2);
                 const V3 tdir = d * k + h.ns * (k * cos1 - cos2);
                 ps.o = hp + tdir * kEpsilon;
                 ps.d = tdir;
@@ -1105,7 +1105,7 @@ RT_D V3 camera_dir(const KParams& P, uint32_t px, uint32_t py, Rng& r) {
     const double x = (2.0 * fx / P.fw - 1.0) * P.tan_x;
     const double y = -(2.0 * fy / P.fh - 1.0) * P.tan_y;
     const V3 dir = (load3(P.cam_right) * x + load3(P.cam_up) * y) + load3(P.cam_fwd) * 1.0;
-    return normalize(dir);
+    return nrm(dir);
 }
 
 // ------------------------------------------------------------ kernels ----
@@ -1502,7 +1502,10 @@ hipError_t launch_ell_rcp(DevShape* shapes, uint32_t n, hipStream_t st) {
 __global__ void fp64_probe_kernel(const double* a, const double* b, double* out, uint32_t n, int op) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    out[i] = op == 0 ? sqrt(a[i]) : (op == 1 ? a[i] / b[i] : dev_quot(a[i], b[i], dev_rcp(b[i])));
+    out[i] = op == 0 ? sqrt(a[i])
+           : op == 1 ? a[i] / b[i]
+           : op == 2 ? dev_quot(a[i], b[i], dev_rcp(b[i]))
+           : op == 3 ? dev_sqrt(a[i]) : dev_inv_len(a[i]);
 }
 
 // ------------------------------------------------------------- launch ----

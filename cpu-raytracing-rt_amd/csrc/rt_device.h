@@ -253,6 +253,37 @@ RT_D double dev_quotz(double x, double y, double r) {
     return x == 0.0 ? x * r : q;
 }
 
+// sqrt(x) as the device computes it (render.hip ISA): for x < 2^-767 the compiler
+// pre-scales by 2^256, and 0 / +inf pass through a class test; for x in
+// [2^-767, +inf) both steps are identities and the result is this core — rsq,
+// two products and six FMAs — bit for bit.  Other x take the library sqrt (a
+// divergent branch that whole waves skip).  dev_inv_len(dd) = 1 / sqrt(dd) of
+// normalize (cgmath normalize_to(1)) with the split division where the length
+// is in dir_ok's range.  Checked against the host (test_dev_sqrt_matches_host).
+RT_D double sqrt_core(double x) {
+    double r = __builtin_amdgcn_rsq(x);
+    double g = x * r, h = r * 0.5;
+    const double e = fma(-h, g, 0.5);
+    g = fma(g, e, g);
+    h = fma(h, e, h);
+    double d = fma(-g, g, x);
+    g = fma(d, h, g);
+    d = fma(-g, g, x);
+    return fma(d, h, g);
+}
+RT_D double dev_sqrt(double x) {
+    if (x >= 0x1p-767 && x < INFINITY) return sqrt_core(x);
+    return sqrt(x);
+}
+RT_D double dev_inv_len(double dd) {
+    if (dd >= 0x1p-700 && dd <= 0x1p700) {  // length in [2^-350, 2^350]
+        const double m = sqrt_core(dd);
+        return dev_quot(1.0, m, dev_rcp(m));
+    }
+    return 1.0 / sqrt(dd);
+}
+RT_D V3 nrm(V3 v) { return v * dev_inv_len(dot(v, v)); }  // normalize (rt_math.h), device form
+
 // per-axis reciprocals of a ray direction (shared by every slab test of a ray):
 // dev_rcp(d) for dev_quot; ok bit i <=> dir_ok(d[i])
 struct Rcp3 {
@@ -460,7 +491,7 @@ RT_D int ell_coef(const Radii& R, V3 o, V3 d, double& t1o, double& t2o) {
     double c = dot(oo, oo), b = dot(oo, dd), a = dot(dd, dd);
     double disc = b * b - a * (c - 1.0);
     if (disc < 0.0) return 0;
-    double ds = sqrt(disc);
+    double ds = dev_sqrt(disc);
     double t1 = (-b + ds) / a, t2 = (-b - ds) / a;
     if (t2 < t1) { double tmp = t1; t1 = t2; t2 = tmp; }
     t1o = t1; t2o = t2;
@@ -470,7 +501,7 @@ RT_D int ell_coef(const Radii& R, V3 o, V3 d, double& t1o, double& t2o) {
 }
 RT_D V3 ell_normal(const Radii& R, V3 o, V3 d, double t) {  // ellipsoid.rs:26,29
     V3 p = o + d * t;
-    return normalize(div_radii(div_radii(p, R), R));
+    return nrm(div_radii(div_radii(p, R), R));
 }
 
 // Triangle::intersection (triangle.rs:49-80) up to (u, v, t); normals later.
@@ -493,7 +524,7 @@ struct Hit { double t; V3 ng, ns; bool inside; };
 
 RT_D Hit rotated(const Hit& h, Quat q) {  // with_rotated_normal (intersections.rs:32-39)
     const bool ident = is_identity(q);
-    return Hit{h.t, normalize(rotate_fast(q, ident, h.ng)), normalize(rotate_fast(q, ident, h.ns)), h.inside};
+    return Hit{h.t, nrm(rotate_fast(q, ident, h.ng)), nrm(rotate_fast(q, ident, h.ns)), h.inside};
 }
 
 }  // namespace rt

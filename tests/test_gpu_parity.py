@@ -104,6 +104,26 @@ def test_dev_quot_matches_host(rt):
         assert np.array_equal(rt.probe_fp64(1, x, y), x / y)
 
 
+def test_dev_sqrt_matches_host(rt):
+    """The kernels' sqrt core (rsq + Newton steps without the compiler's range
+    scaling) and normalize's 1 / sqrt(d.d) give the host's bits on and off their
+    fast ranges (rt_device.h dev_sqrt, dev_inv_len)."""
+    rng = np.random.default_rng(3)
+    x = np.ldexp(1.0 + rng.random(1 << 20), rng.integers(-1074, 1024, 1 << 20))
+    x = np.concatenate([x, rng.random(1 << 18), 1.0 + rng.random(1 << 18) * 2.0,
+                        [0.0, -0.0, np.inf, -1.0, np.nan, 5e-324, 2.0 ** -767, np.nextafter(2.0 ** -767, 0),
+                         2.0 ** -700, 2.0 ** 700, np.nextafter(2.0 ** 700, np.inf), 1.0, 4.0]])
+    with np.errstate(invalid="ignore", divide="ignore", over="ignore"):
+        want_s, want_i = np.sqrt(x), 1.0 / np.sqrt(x)
+    got_s, got_i = rt.probe_fp64(3, x), rt.probe_fp64(4, x)
+    ok = ~np.isnan(want_s)
+    assert np.array_equal(got_s[ok].view(np.uint64), want_s[ok].view(np.uint64))
+    assert np.isnan(got_s[~ok]).all()
+    ok = ~np.isnan(want_i)
+    assert np.array_equal(got_i[ok].view(np.uint64), want_i[ok].view(np.uint64))
+    assert np.isnan(got_i[~ok]).all()
+
+
 def test_cornell_small(cornell):
     desc, params, g, o = cornell
     _compare(g, o, params.replace(width=48, height=40, spp=4))
