@@ -158,6 +158,8 @@ hipError_t ws_end(rt_scene* s, hipStream_t st) { return hipEventRecord(s->ws_don
 int check_params(const rt_render_params* p) {
     if (!p) return set_error(RT_ERR_INVALID, "params is NULL");
     if (p->width == 0 || p->height == 0) return set_error(RT_ERR_INVALID, "width/height must be > 0");
+    // the path kernel packs a wave-tile's pixel origin into 16 + 16 bits (render.hip store_unit)
+    if (p->width > 65535 || p->height > 65535) return set_error(RT_ERR_INVALID, "width/height must be <= 65535");
     if (p->spp == 0) return set_error(RT_ERR_INVALID, "spp must be > 0");
     if (p->ray_depth > 255) return set_error(RT_ERR_INVALID, "ray_depth is a u8 in the reference (scene.rs:85)");
     if (p->fov_axis != RT_FOV_X && p->fov_axis != RT_FOV_Y) return set_error(RT_ERR_INVALID, "bad fov_axis");

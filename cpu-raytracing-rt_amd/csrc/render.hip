@@ -1148,6 +1148,40 @@ RT_D const T* opaque(const T* p) {
 #endif
 }
 
+// A wave-tile (tile slot, sample chunk, 8x8 quadrant) in frame coordinates.
+struct UnitGeo {
+    uint32_t qx0, qy0, s0, nrows, oslot;  // quadrant origin, first sample, sample rows, output slot
+    uint32_t quad;
+    bool tile_ok;
+};
+RT_D UnitGeo unit_geo(const KParams& P, uint32_t unit) {
+    UnitGeo g;
+    g.quad = unit & 3u;
+    const uint32_t sci = unit >> 2;  // slot * chunks + chunk
+    const uint32_t slot = sci / P.chunks, chunk = sci % P.chunks;
+    const uint64_t tile = (uint64_t)P.rank + (uint64_t)slot * P.world;
+    g.tile_ok = tile < P.n_tiles;
+    g.qx0 = (uint32_t)(tile % P.tiles_x) * RT_TILE + (g.quad & 1u) * 8u;
+    g.qy0 = (uint32_t)(tile / P.tiles_x) * RT_TILE + (g.quad >> 1) * 8u;
+    g.s0 = chunk * P.chunk_spp;
+    g.nrows = min(P.spp, g.s0 + P.chunk_spp) - g.s0;
+    g.oslot = P.chunks == 1 ? slot : sci;  // out[slot] (means) or part[sci] (chunk sums)
+    return g;
+}
+// an open wave-tile's LDS entry: first stream row, qx0 | qy0 << 16, first
+// sample, rows, output slot, tile_ok | quad << 1
+constexpr uint32_t kUQ = 8, kUW = 6;
+RT_D void store_unit(uint32_t* e, uint32_t first, const UnitGeo& g) {
+    e[0] = first; e[1] = g.qx0 | (g.qy0 << 16); e[2] = g.s0; e[3] = g.nrows; e[4] = g.oslot;
+    e[5] = (g.tile_ok ? 1u : 0u) | (g.quad << 1);
+}
+// entry index of the open wave-tile holding stream row `row` (wave-uniform)
+RT_D uint32_t unit_of_row(const uint32_t* uq, uint32_t uq_back, uint32_t row) {
+    uint32_t i = uq_back - 1u;
+    while (uq[(i % kUQ) * kUW] > row) --i;
+    return i % kUQ;
+}
+
 template <bool ST, bool HIT, int WAVES, bool RES>
 __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams Pv,
                                                      const DevScene* __restrict__ Sg,
@@ -1159,8 +1193,9 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
     __shared__ uint32_t s_n[kShort * kWave];
     __shared__ double s_t[kShort * kWave];
     __shared__ uint32_t s_cnt[kRing];  // finished paths per ring row
-    // camera rays of the next kCamSlots units, [component][slot] (fused kernel only)
+    // camera rays of the next kCamSlots paths, [component][slot] (fused kernel only)
     __shared__ double s_cam[RES ? 1 : 3 * kCamSlots];
+    __shared__ uint32_t s_uq[kUQ * kUW];  // open wave-tiles (store_unit)
     const uint32_t lane = threadIdx.x;
     auto stk = make_stack<RES>(s_n, s_t, 0u, (uint64_t)blockIdx.x * kWave, spill_n, spill_t,
                            gridDim.x * kWave);
@@ -1175,194 +1210,211 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
     if (lane < kPhN) g_phase[lane] = 0;
     __syncthreads();
 #endif
-    for (;;) {  // wave-tiles; every wave leaves once the queue passes n_units
-        const unsigned long long ph_tile = PH_T();
-        uint32_t u = 0;
-        if (lane == 0) u = atomicAdd(queue, 1u);
-        const uint32_t unit = __builtin_amdgcn_readfirstlane(u);
-        if (unit >= n_units) break;
-        const uint32_t quad = unit & 3u, sci = unit >> 2;  // sci = slot * chunks + chunk
-        const uint32_t slot = sci / Pt.chunks, chunk = sci % Pt.chunks;
-        const uint64_t tile = (uint64_t)Pt.rank + (uint64_t)slot * Pt.world;
-        const bool tile_ok = tile < Pt.n_tiles;
-        const uint32_t qx0 = (uint32_t)(tile % Pt.tiles_x) * RT_TILE + (quad & 1u) * 8u;
-        const uint32_t qy0 = (uint32_t)(tile / Pt.tiles_x) * RT_TILE + (quad >> 1) * 8u;
-        const uint32_t s0 = chunk * Pt.chunk_spp;
-        const uint32_t nrows = min(Pt.spp, s0 + Pt.chunk_spp) - s0, total = nrows * kWave;
-        if (lane < kRing) s_cnt[lane] = 0;
-        __syncthreads();
-        V3 sum = v3(0.0, 0.0, 0.0);
-        uint32_t base = 0, next = 0, witers = 0;  // wave-uniform schedule
-        uint32_t cam_end = 0;  // camera rays of units [cam_end - kCamSlots, cam_end) are in s_cam
-        bool busy = false;
-        uint32_t cur = 0, s = 0, b = 0;
-        uint64_t pixel = 0;
-        PathState ps;
-        Rng rng;
-        SegQuery q;
-        q.T.live = false;
-        bool inq = false;  // this lane's segment query is under way
-        for (;;) {
-            // fields s_load'ed where used (see opaque), for both register budgets
-            // (C3 at 64 spp: 315.6 vs 325.9 ms with the by-value kernel
-            // arguments of the 4-wave kernel, whose loads were hoisted into
-            // SGPRs and spilled)
+    // The wave's work is one stream of sample rows: wave-tiles pulled from the
+    // queue append their rows to it (s_uq holds the open ones), idle lanes take
+    // the next (row, pixel) paths across wave-tile boundaries, and rows commit
+    // in stream order, each lane adding its own pixel's radiance; the last row
+    // of the oldest open wave-tile writes that tile's sums.  Lanes never wait
+    // for a wave-tile's longest path before starting the next one.
+    const unsigned long long ph_tile = PH_T();
+    if (lane < kRing) s_cnt[lane] = 0;
+    __syncthreads();
+    V3 sum = v3(0.0, 0.0, 0.0);
+    uint32_t base = 0, next = 0, witers = 0;  // wave-uniform: next row to commit, next path to hand out
+    uint32_t open_end = 0;                    // rows of the wave-tiles pulled so far
+    uint32_t uq_front = 0, uq_back = 0;       // open wave-tiles: s_uq entries [uq_front, uq_back)
+    bool drained = false;                     // the queue is empty
+    uint32_t cam_end = 0;  // camera rays of paths [cam_end - kCamSlots, cam_end) are in s_cam
+    bool busy = false;
+    uint32_t cur = 0, s = 0, b = 0;
+    uint64_t pixel = 0;
+    PathState ps;
+    Rng rng;
+    SegQuery q;
+    q.T.live = false;
+    bool inq = false;  // this lane's segment query is under way
+    for (;;) {
+        // fields s_load'ed where used (see opaque), for both register budgets
+        // (C3 at 64 spp: 315.6 vs 325.9 ms with the by-value kernel
+        // arguments of the 4-wave kernel, whose loads were hoisted into
+        // SGPRs and spilled)
 #ifndef RT_SCENE_BYVAL4  // ablation build: by-value arguments for the 4-wave kernel
-            constexpr bool kByPtr = true;
+        constexpr bool kByPtr = true;
 #else
-            constexpr bool kByPtr = WAVES == 3;
+        constexpr bool kByPtr = WAVES == 3;
 #endif
-            const DevScene& S = kByPtr ? *opaque(Sg) : Sv;
-            const KParams& P = kByPtr ? *opaque(Pg) : Pv;
-            const Scales sc{P.scale01, P.scale11};
-            // hand the next units to idle lanes, in lane order, inside the ring window
-            const uint32_t limit = min(total, (base + kRing) * kWave);
-            const uint64_t idle = __ballot(!busy);
-            const unsigned long long ph_a = PH_T();
-            if (next < limit && idle) {
-                if constexpr (!RES) {
-                    // Camera rays for the units this trip may hand out, one sample row
-                    // (64 units, lane = pixel) at a time with every lane active, instead
-                    // of per path start with only the idle lanes.  Rows
-                    // [cam_end - 128, cam_end - 64) are overwritten only once consumed.
-                    const uint32_t need = min(limit, next + (uint32_t)__popcll(idle));
-                    while (cam_end < need) {
-                        const uint32_t px = qx0 + (lane & 7u), py = qy0 + (lane >> 3);
-                        V3 dir = v3(0.0, 0.0, 0.0);
-                        if (tile_ok && px < P.width && py < P.height) {
-                            Rng cr;
-                            rng_init(cr, P.seed, (uint64_t)py * P.width + px, s0 + cam_end / kWave);
-                            dir = camera_dir(P, px, py, cr);
-                        }
-                        const uint32_t slot = (cam_end + lane) % kCamSlots;
-                        s_cam[slot] = dir.x; s_cam[kCamSlots + slot] = dir.y; s_cam[2 * kCamSlots + slot] = dir.z;
-                        cam_end += kWave;
+        const DevScene& S = kByPtr ? *opaque(Sg) : Sv;
+        const KParams& P = kByPtr ? *opaque(Pg) : Pv;
+        const Scales sc{P.scale01, P.scale11};
+        const uint64_t idle = __ballot(!busy);
+        const unsigned long long ph_a = PH_T();
+        // pull wave-tiles until the rows the idle lanes could take exist (inside the
+        // commit window of kRing rows, at most kUQ open)
+        const uint32_t window = (base + kRing) * kWave;
+        const uint32_t want = min(window, next + (uint32_t)__popcll(idle));
+        while (!drained && open_end * kWave < want && uq_back - uq_front < kUQ) {
+            uint32_t u = 0;
+            if (lane == 0) u = atomicAdd(queue, 1u);
+            const uint32_t unit = __builtin_amdgcn_readfirstlane(u);
+            if (unit >= n_units) { drained = true; break; }
+            const UnitGeo g = unit_geo(Pt, unit);
+            if (lane == 0) store_unit(s_uq + (uq_back % kUQ) * kUW, open_end, g);
+            open_end += g.nrows;
+            ++uq_back;
+            __syncthreads();
+        }
+        const uint32_t limit = min(window, open_end * kWave);
+        if (next < limit && idle) {
+            if constexpr (!RES) {
+                // Camera rays for the paths this trip may hand out, one sample row
+                // (64 paths, lane = pixel) at a time with every lane active, instead
+                // of per path start with only the idle lanes.  Rows
+                // [cam_end - 128, cam_end - 64) are overwritten only once consumed.
+                const uint32_t need = min(limit, next + (uint32_t)__popcll(idle));
+                while (cam_end < need) {
+                    const uint32_t row = cam_end / kWave;
+                    const uint32_t* e = s_uq + unit_of_row(s_uq, uq_back, row) * kUW;
+                    const uint32_t qxy = e[1];
+                    const uint32_t px = (qxy & 0xFFFFu) + (lane & 7u), py = (qxy >> 16) + (lane >> 3);
+                    V3 dir = v3(0.0, 0.0, 0.0);
+                    if ((e[5] & 1u) && px < P.width && py < P.height) {
+                        Rng cr;
+                        rng_init(cr, P.seed, (uint64_t)py * P.width + px, e[2] + (row - e[0]));
+                        dir = camera_dir(P, px, py, cr);
                     }
-                    __syncthreads();
+                    const uint32_t slot = (cam_end + lane) % kCamSlots;
+                    s_cam[slot] = dir.x; s_cam[kCamSlots + slot] = dir.y; s_cam[2 * kCamSlots + slot] = dir.z;
+                    cam_end += kWave;
                 }
-                const uint32_t k = (uint32_t)__popcll(idle & below);
-                if (!busy && next + k < limit) {
-                    cur = next + k;
-                    const uint32_t col = cur % kWave;
-                    const uint32_t px = qx0 + (col & 7u), py = qy0 + (col >> 3);
-                    s = s0 + cur / kWave;
-                    if (tile_ok && px < P.width && py < P.height) {
-                        // Camera::fuzzy_ray + raytrace (camera.rs:48-55, raytrace.rs:8-10)
-                        pixel = (uint64_t)py * P.width + px;
-                        rng_init(rng, P.seed, pixel, s);
-                        ps.o = load3(P.cam_pos);
-                        if constexpr (!RES) {  // precomputed above: block 0 consumed
-                            const uint32_t slot = cur % kCamSlots;
-                            ps.d = v3(s_cam[slot], s_cam[kCamSlots + slot], s_cam[2 * kCamSlots + slot]);
-                            rng.blk = 1;
-                        } else {
-                            ps.d = camera_dir(P, px, py, rng);
-                        }
-                        ps.T = v3(1.0, 1.0, 1.0);
-                        ps.L = v3(0.0, 0.0, 0.0);
-                        ps.pend = false;
-                        b = 0;
-                        busy = true;
-                        C.path();
-                    } else {
-                        atomicAdd(&s_cnt[(cur / kWave) % kRing], 1u);  // no pixel: done at once, never read
-                    }
-                }
-                next = min(limit, next + (uint32_t)__popcll(idle));
+                __syncthreads();
             }
-            PH_ADD(kPhAssign, ph_a);
-            bool ends = false;  // this lane's path ends in this trip
-            if constexpr (RES) {
-                // lanes between segments (new paths, continued paths) start their query
-                const unsigned long long ph_b = PH_T();
-                if (busy && !inq && b < depth) {
-                    segment_begin<ST>(S, ps, stk, C, q);
-                    inq = true;
-                }
-                PH_ADDW(kPhIntersect, ph_b);
-                // Triangle traversal, resumable: step while enough lanes are live; once
-                // fewer than kSuspend are, and other lanes wait to shade or to take a new
-                // path, suspend the live ones (their stacks and Trav stay put) so the
-                // waiting lanes run now and rejoin the traversal with their next rays.
-                const unsigned long long ph_t = PH_T();
-                for (;;) {
-                    const uint64_t lv = __ballot(q.T.live);
-                    if (lv == 0) break;
-                    if (__popcll(lv) < kSuspend) {
-                        const bool can_take = next < min(total, (base + kRing) * kWave);
-                        if (__ballot((busy && !q.T.live) || (!busy && can_take))) break;
+            const uint32_t k = (uint32_t)__popcll(idle & below);
+            if (!busy && next + k < limit) {
+                cur = next + k;
+                const uint32_t row = cur / kWave, col = cur % kWave;
+                // the row is in the newest open wave-tile or the one before it (a trip
+                // hands out at most 64 consecutive paths: two rows)
+                const uint32_t eb = (uq_back - 1u) % kUQ;
+                const uint32_t* e = s_uq + (row >= s_uq[eb * kUW] ? eb : (uq_back - 2u) % kUQ) * kUW;
+                const uint32_t qxy = e[1];
+                const uint32_t px = (qxy & 0xFFFFu) + (col & 7u), py = (qxy >> 16) + (col >> 3);
+                s = e[2] + (row - e[0]);
+                if ((e[5] & 1u) && px < P.width && py < P.height) {
+                    // Camera::fuzzy_ray + raytrace (camera.rs:48-55, raytrace.rs:8-10)
+                    pixel = (uint64_t)py * P.width + px;
+                    rng_init(rng, P.seed, pixel, s);
+                    ps.o = load3(P.cam_pos);
+                    if constexpr (!RES) {  // precomputed above: block 0 consumed
+                        const uint32_t slot = cur % kCamSlots;
+                        ps.d = v3(s_cam[slot], s_cam[kCamSlots + slot], s_cam[2 * kCamSlots + slot]);
+                        rng.blk = 1;
+                    } else {
+                        ps.d = camera_dir(P, px, py, rng);
                     }
-                    trav_step<3, 2, ST>(S.tris, ps.o, ps.d, q.rc, q.fast, stk, C, q.T, lv);
+                    ps.T = v3(1.0, 1.0, 1.0);
+                    ps.L = v3(0.0, 0.0, 0.0);
+                    ps.pend = false;
+                    b = 0;
+                    busy = true;
+                    C.path();
+                } else {
+                    atomicAdd(&s_cnt[row % kRing], 1u);  // no pixel: done at once, never read
                 }
-                PH_ADD(kPhTris, ph_t);
-                // lanes whose query finished shade and end (or continue) their segment
-                if (busy && !q.T.live) {
-                    C.step();
-                    bool cont = false;
-                    if (inq) {
-                        int32_t g;
-                        const unsigned long long ph_s = PH_T();
-                        cont = segment_end<ST>(S, P, sc, ps, rng, stk, C, q, g);
-                        PH_ADDW(kPhSegment, ph_s);
-                        if (HIT) hit_ids[(pixel * P.spp + s) * depth + b] = g;
-                        ++b;
-                        inq = false;
-                    }
-                    ends = !cont || b >= depth;
+            }
+            next = min(limit, next + (uint32_t)__popcll(idle));
+        }
+        PH_ADD(kPhAssign, ph_a);
+        bool ends = false;  // this lane's path ends in this trip
+        if constexpr (RES) {
+            // lanes between segments (new paths, continued paths) start their query
+            const unsigned long long ph_b = PH_T();
+            if (busy && !inq && b < depth) {
+                segment_begin<ST>(S, ps, stk, C, q);
+                inq = true;
+            }
+            PH_ADDW(kPhIntersect, ph_b);
+            // Triangle traversal, resumable: step while enough lanes are live; once
+            // fewer than kSuspend are, and other lanes wait to shade or to take a new
+            // path, suspend the live ones (their stacks and Trav stay put) so the
+            // waiting lanes run now and rejoin the traversal with their next rays.
+            const unsigned long long ph_t = PH_T();
+            for (;;) {
+                const uint64_t lv = __ballot(q.T.live);
+                if (lv == 0) break;
+                if (__popcll(lv) < kSuspend) {
+                    const uint32_t win = (base + kRing) * kWave;
+                    const bool can_take = next < min(win, open_end * kWave) || (!drained && next < win);
+                    if (__ballot((busy && !q.T.live) || (!busy && can_take))) break;
                 }
-            } else if (busy) {  // fused: one whole segment of every live path
+                trav_step<3, 2, ST>(S.tris, ps.o, ps.d, q.rc, q.fast, stk, C, q.T, lv);
+            }
+            PH_ADD(kPhTris, ph_t);
+            // lanes whose query finished shade and end (or continue) their segment
+            if (busy && !q.T.live) {
                 C.step();
                 bool cont = false;
-                if (b < depth) {
+                if (inq) {
                     int32_t g;
                     const unsigned long long ph_s = PH_T();
-                    cont = segment<ST>(S, P, sc, ps, rng, stk, C, g, b + 1 < depth);
+                    cont = segment_end<ST>(S, P, sc, ps, rng, stk, C, q, g);
                     PH_ADDW(kPhSegment, ph_s);
                     if (HIT) hit_ids[(pixel * P.spp + s) * depth + b] = g;
                     ++b;
+                    inq = false;
                 }
-                if (!cont || b >= depth) {
-                    if (HIT) for (uint32_t k = b; k < depth; ++k) hit_ids[(pixel * P.spp + s) * depth + k] = RT_HIT_NONE;
-                    const uint32_t r = (cur / kWave) % kRing;
-                    double* rp = ring + ((uint64_t)r * kWave + cur % kWave) * 3;
-                    rp[0] = ps.L.x; rp[1] = ps.L.y; rp[2] = ps.L.z;
-                    atomicAdd(&s_cnt[r], 1u);
-                    busy = false;
-                }
+                ends = !cont || b >= depth;
             }
-            if (RES && ends) {
-                if (HIT) for (uint32_t k = b; k < depth; ++k) hit_ids[(pixel * P.spp + s) * depth + k] = RT_HIT_NONE;
-                const uint32_t r = (cur / kWave) % kRing;
-                double* rp = ring + ((uint64_t)r * kWave + cur % kWave) * 3;
-                rp[0] = ps.L.x; rp[1] = ps.L.y; rp[2] = ps.L.z;
-                atomicAdd(&s_cnt[r], 1u);
-                busy = false;
+        } else if (busy) {  // fused: one whole segment of every live path
+            C.step();
+            bool cont = false;
+            if (b < depth) {
+                int32_t g;
+                const unsigned long long ph_s = PH_T();
+                cont = segment<ST>(S, P, sc, ps, rng, stk, C, g, b + 1 < depth);
+                PH_ADDW(kPhSegment, ph_s);
+                if (HIT) hit_ids[(pixel * P.spp + s) * depth + b] = g;
+                ++b;
             }
-            ++witers;
-            // commit complete rows in sample order (ring stores visible to the wave)
-            const unsigned long long ph_c = PH_T();
-            __syncthreads();
-            while (base < nrows && s_cnt[base % kRing] == (uint32_t)kWave) {
-                const double* rp = ring + ((uint64_t)(base % kRing) * kWave + lane) * 3;
-                sum = sum + v3(rp[0], rp[1], rp[2]);
-                __syncthreads();
-                if (lane == 0) s_cnt[base % kRing] = 0;
-                __syncthreads();
-                ++base;
-            }
-            PH_ADD(kPhCommit, ph_c);
-            if (base >= nrows) break;
+            ends = !cont || b >= depth;
         }
-        const uint32_t lx = (quad & 1u) * 8u + (lane & 7u), ly = (quad >> 1) * 8u + (lane >> 3);
-        const bool own = tile_ok && qx0 + (lane & 7u) < Pt.width && qy0 + (lane >> 3) < Pt.height;
-        V3 res = own ? (Pt.chunks == 1 ? sum / (double)Pt.spp : sum) : v3(0.0, 0.0, 0.0);  // main.rs:104
-        double* o = Pt.chunks == 1 ? out + ((uint64_t)slot * kBlock + ly * RT_TILE + lx) * 3
-                                  : part + ((uint64_t)sci * kBlock + ly * RT_TILE + lx) * 3;
-        o[0] = res.x; o[1] = res.y; o[2] = res.z;
-        wave_flush<ST>(C, stats, witers);
-        C.zero();
-        PH_ADD(kPhTile, ph_tile);
+        if (ends) {
+            if (HIT) for (uint32_t k = b; k < depth; ++k) hit_ids[(pixel * P.spp + s) * depth + k] = RT_HIT_NONE;
+            const uint32_t r = (cur / kWave) % kRing;
+            double* rp = ring + ((uint64_t)r * kWave + cur % kWave) * 3;
+            rp[0] = ps.L.x; rp[1] = ps.L.y; rp[2] = ps.L.z;
+            atomicAdd(&s_cnt[r], 1u);
+            busy = false;
+        }
+        ++witers;
+        // commit complete rows in stream order (ring stores visible to the wave);
+        // the last row of the oldest open wave-tile writes its per-pixel sums
+        const unsigned long long ph_c = PH_T();
+        __syncthreads();
+        while (base < open_end && s_cnt[base % kRing] == (uint32_t)kWave) {
+            const double* rp = ring + ((uint64_t)(base % kRing) * kWave + lane) * 3;
+            sum = sum + v3(rp[0], rp[1], rp[2]);
+            __syncthreads();
+            if (lane == 0) s_cnt[base % kRing] = 0;
+            __syncthreads();
+            const uint32_t* e = s_uq + (uq_front % kUQ) * kUW;
+            if (base + 1u == e[0] + e[3]) {  // main.rs:104 for this wave-tile's pixels
+                const uint32_t qxy = e[1], quad = e[5] >> 1;
+                const uint32_t lx = (quad & 1u) * 8u + (lane & 7u), ly = (quad >> 1) * 8u + (lane >> 3);
+                const bool own = (e[5] & 1u) && (qxy & 0xFFFFu) + (lane & 7u) < Pt.width &&
+                                 (qxy >> 16) + (lane >> 3) < Pt.height;
+                const V3 res = own ? (Pt.chunks == 1 ? sum / (double)Pt.spp : sum) : v3(0.0, 0.0, 0.0);
+                double* o = (Pt.chunks == 1 ? out : part) + ((uint64_t)e[4] * kBlock + ly * RT_TILE + lx) * 3;
+                o[0] = res.x; o[1] = res.y; o[2] = res.z;
+                sum = v3(0.0, 0.0, 0.0);
+                ++uq_front;
+            }
+            ++base;
+        }
+        PH_ADD(kPhCommit, ph_c);
+        if (drained && uq_front == uq_back) break;  // every pulled wave-tile written
     }
+    wave_flush<ST>(C, stats, witers);
+    PH_ADD(kPhTile, ph_tile);
 #ifdef RT_PHASES
     if (ST && lane < kPhN) atomicAdd(&stats[kPhaseWord0 + lane], g_phase[lane]);
 #endif
