@@ -36,13 +36,17 @@ constexpr int kPhaseWord0 = 16;   // RT_PHASES builds: region cycles + loop coun
 
 // Chunk count for a frame: a function of (W, H, spp) only, so the image does not
 // depend on the number of GPUs.  Doubles while the frame has < kChunkLanes
-// work units, capped at spp and kMaxChunks, then trimmed so no chunk is empty.
-constexpr uint64_t kChunkLanes = 16000000;
+// work units or the chunks would still hold >= kMinChunkSpp samples (many short
+// wave-tiles balance the ranks of a multi-GPU frame; the path kernel streams
+// rows across wave-tiles, so short ones cost no drain), capped at spp and
+// kMaxChunks, then trimmed so no chunk is empty.
+constexpr uint64_t kChunkLanes = 32000000;
+constexpr uint32_t kMinChunkSpp = 16;
 constexpr uint32_t kMaxChunks = 64;
 inline void sample_chunks(uint32_t W, uint32_t H, uint32_t spp, uint32_t& chunks, uint32_t& chunk_spp) {
     const uint64_t px = (uint64_t)W * H;
     uint32_t k = 1;
-    while (k * 2 <= spp && k < kMaxChunks && px * k < kChunkLanes) k *= 2;
+    while (k * 2 <= spp && k < kMaxChunks && (px * k < kChunkLanes || spp / (k * 2) >= kMinChunkSpp)) k *= 2;
     chunk_spp = (spp + k - 1) / k;
     chunks = (spp + chunk_spp - 1) / chunk_spp;
 }

@@ -191,12 +191,13 @@ def test_chunked_sum_is_reassociation_only(rt, orc, scene_text):
 
 
 @pytest.mark.parametrize("w,h,spp,want", [
-    (1920, 1080, 256, (8, 32)),     # C2/C3: 16.6M work units
-    (3840, 2160, 1024, (2, 512)),   # C4
+    (1920, 1080, 256, (16, 16)),    # C2/C3: 33M work units
+    (3840, 2160, 1024, (64, 16)),   # C4: 16-spp chunks
+    (1920, 1080, 64, (16, 4)),      # C5
     (256, 256, 64, (64, 1)),        # C1: capped at kMaxChunks
     (48, 32, 4, (4, 1)),
     (20, 12, 5, (3, 2)),            # 4 runs of 2 would leave one empty: trimmed to 3
-    (4000, 4000, 9, (1, 9)),        # already >= 16M pixels
+    (4000, 4000, 9, (2, 5)),        # 16M pixels: two runs reach 32M work units
     (7, 3, 1, (1, 1)),
 ])
 def test_sample_chunk_rule(rt, w, h, spp, want):
