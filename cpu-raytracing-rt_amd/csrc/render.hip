@@ -942,22 +942,30 @@ RT_D void segment_begin(const DevScene& S, const PathState& ps, Stk& stk, Cnt<ST
 
 // One segment of raytrace_impl (raytrace.rs:12-60) in throughput form, from
 // the closest-hit result on.  Returns true when the path continues with the
-// updated ray.
+// updated ray.  `last`: this is the path's last segment (raytrace_impl with
+// left == 1).
 template <bool ST, class Stk, bool SLT = false>
 RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, PathState& ps, Rng& rng,
                         Stk& stk, Cnt<ST>& C, bool hit, const Hit& h, uint32_t mat, int32_t gid,
-                        int32_t& hit_gid, bool more = false) {
+                        int32_t& hit_gid, bool more, bool last) {
     if (!hit) {
         hit_gid = RT_HIT_MISS;
         ps.L = ps.L + mul(ps.T, load3(P.bg));
         return false;
     }
     hit_gid = gid;
-    rng_align(rng);   // shading draws start on a block boundary (oracle.c rng_align)
-    rng_top_up(rng);  // every hit lane here: a coherent refill point
     const DevMaterial& m = S.mats[mat];
     const V3 col = load3(m.color);
     ps.L = ps.L + mul(ps.T, load3(m.emission));
+    // On the last segment the rest of the shading (direction, light pdf, weight)
+    // only feeds raytrace_impl(left - 1) == 0: a throughput nothing reads again and
+    // draws no later segment makes.  The product stops here (the radiance and hit
+    // ids are the same bits); the stats build (ST) still runs it, so the work
+    // counters stay the oracle's (whose light query on the last bounce the SURVEY
+    // byte model counts).
+    if (!ST && last) return false;
+    rng_align(rng);   // shading draws start on a block boundary (oracle.c rng_align)
+    rng_top_up(rng);  // every hit lane here: a coherent refill point
     const V3 o = ps.o, d = ps.d;
     if (m.kind == RT_MAT_DIFFUSE) {  // :16-34
         V3 pos = o + d * h.t;
@@ -1051,7 +1059,9 @@ RT_D bool segment_end(const DevScene& S, const KParams& P, const Scales& sc, Pat
     Hit h; uint32_t mat = 0; int32_t gid = 0;
     take_tri(q.best, q.T.valid, q.T.best, q.T.bu, q.T.bv, q.T.prim);
     const bool hit = intersect_tail<ST>(S, q.best, ps.o, ps.d, C, h, mat, gid);
-    return segment_shade<ST>(S, P, sc, ps, rng, stk, C, hit, h, mat, gid, hit_gid);
+    // (no last-segment shortcut here: it cost the 4-wave resumable kernel's
+    // register allocation more than it saved, C3 +1.5%)
+    return segment_shade<ST>(S, P, sc, ps, rng, stk, C, hit, h, mat, gid, hit_gid, false, false);
 }
 
 // the fused form: one whole segment (scene_intersect to completion, then shade)
@@ -1071,7 +1081,7 @@ RT_D bool segment(const DevScene& S, const KParams& P, const Scales& sc, PathSta
         ps.pend = false;
     }
     PH_ADDW(kPhIntersect, ph0);
-    return segment_shade<ST, Stk, true>(S, P, sc, ps, rng, stk, C, hit, h, mat, gid, hit_gid, more);
+    return segment_shade<ST, Stk, true>(S, P, sc, ps, rng, stk, C, hit, h, mat, gid, hit_gid, more, !more);
 }
 
 template <bool ST>

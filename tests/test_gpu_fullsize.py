@@ -39,6 +39,8 @@ def test_full_frame_rows_match_oracle(rt, orc, monkeypatch, name, rows):
     desc, params = _workload(rt, name)
     scene = rt.Scene(desc)
     img, _, st = scene.generate_image(params, stats=True)
+    # the timed product kernel (no stats) renders the same bits
+    assert np.array_equal(scene.generate_image(params)[0], img)
     assert img.shape == (params.height, params.width, 3)
     assert np.isfinite(img).all() and (img >= 0).all()
     assert st["paths"] == params.width * params.height * params.spp

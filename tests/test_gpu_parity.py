@@ -48,6 +48,11 @@ def _compare(gpu_scene, ora_scene, params):
     assert np.array_equal(g_hits, o_hits), f"hit ids differ at {np.argwhere(g_hits != o_hits)[:5]}"
     assert np.array_equal(g_hits, r_hits)
     assert np.array_equal(g_img, o_img), f"max |d| {np.max(np.abs(g_img - o_img))}"
+    # the product instances (no stats: the timed kernel, and hit ids without stats)
+    p_img, p_hits, _ = gpu_scene.generate_image(params, hit_ids=True)
+    assert np.array_equal(p_hits, o_hits) and np.array_equal(p_img, o_img)
+    p_img, _, _ = gpu_scene.generate_image(params)
+    assert np.array_equal(p_img, o_img), f"product kernel: max |d| {np.max(np.abs(p_img - o_img))}"
     np.testing.assert_allclose(g_img, r_img, rtol=REL_TOL, atol=1e-300)
     for k in ("paths", "segments", "aabb_tests", "tri_tests", "shape_tests", "shaded_hits",
               "light_queries", "light_hits"):
