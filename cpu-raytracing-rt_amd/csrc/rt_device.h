@@ -423,8 +423,10 @@ RT_D bool plane_t(V3 n, V3 o, V3 d, double& t, uint32_t& aux) {
     return true;
 }
 
-// intersect_box_coef (box.rs:75-115). Entry/exit as (t, sign, dim).
-struct Bpi { double t; double sign; int dim; };
+// intersect_box_coef (box.rs:75-115). Entry/exit as (t, face): face = dim | 4 when
+// the plane's normal sign is +1 (one 32-bit word, so each max/min update of the
+// three axes selects three registers instead of five)
+struct Bpi { double t; uint32_t face; };
 // FD: shape_fast holds (d has no zero component; every quotient exact by dev_quotz)
 template <bool FD = false>
 RT_D int box_coef(V3 s, V3 o, V3 d, const Rcp3& rc, Bpi& en, Bpi& ex) {
@@ -437,12 +439,13 @@ RT_D int box_coef(V3 s, V3 o, V3 d, const Rcp3& rc, Bpi& en, Bpi& ex) {
         const double ri = comp(rc.r, i);
         double t1 = FD ? dev_quotz(si - oi, di, ri) : (si - oi) / di;
         double t2 = FD ? dev_quotz(-si - oi, di, ri) : (-si - oi) / di;
-        double a, b, nrm;
-        if (t1 < t2) { a = t1; b = t2; nrm = 1.0; } else { a = t2; b = t1; nrm = -1.0; }
-        if (!have) { en = Bpi{a, nrm, i}; ex = Bpi{b, nrm, i}; have = true; }
+        double a, b;
+        uint32_t f;
+        if (t1 < t2) { a = t1; b = t2; f = (uint32_t)i | 4u; } else { a = t2; b = t1; f = (uint32_t)i; }
+        if (!have) { en = Bpi{a, f}; ex = Bpi{b, f}; have = true; }
         else {
-            if (!(a < en.t)) en = Bpi{a, nrm, i};   // BoxPlaneIntersection::max (box.rs:57-59)
-            if (b < ex.t) ex = Bpi{b, nrm, i};      // BoxPlaneIntersection::min (box.rs:60-62)
+            if (!(a < en.t)) en = Bpi{a, f};   // BoxPlaneIntersection::max (box.rs:57-59)
+            if (b < ex.t) ex = Bpi{b, f};      // BoxPlaneIntersection::min (box.rs:60-62)
         }
     }
     if (!have) return 0;
@@ -452,14 +455,15 @@ RT_D int box_coef(V3 s, V3 o, V3 d, const Rcp3& rc, Bpi& en, Bpi& ex) {
     return 0;
 }
 RT_D V3 bpi_normal(const Bpi& p) {  // box.rs:64-72
-    if (p.dim == 0) return v3(p.sign, 0.0, 0.0);
-    if (p.dim == 1) return v3(0.0, p.sign, 0.0);
-    return v3(0.0, 0.0, p.sign);
+    const double sign = (p.face & 4u) ? 1.0 : -1.0;
+    const uint32_t dim = p.face & 3u;
+    if (dim == 0) return v3(sign, 0.0, 0.0);
+    if (dim == 1) return v3(0.0, sign, 0.0);
+    return v3(0.0, 0.0, sign);
 }
+RT_D int bpi_dim(const Bpi& p) { return (int)(p.face & 3u); }
 // aux encodes the returned face: bits0-1 dim, bit2 sign(+1), bit3 inside
-RT_D uint32_t bpi_aux(const Bpi& p, bool inside) {
-    return (uint32_t)p.dim | (p.sign > 0.0 ? 4u : 0u) | (inside ? 8u : 0u);
-}
+RT_D uint32_t bpi_aux(const Bpi& p, bool inside) { return p.face | (inside ? 8u : 0u); }
 RT_D V3 aux_box_normal(uint32_t aux) {
     double s = (aux & 4u) ? 1.0 : -1.0;
     uint32_t dim = aux & 3u;
