@@ -275,6 +275,18 @@ bool path_resume(const rt_scene* s) {
     return s->info.bvh_nodes[2] > kDeepSceneNodes;
 }
 
+// Triangle-only scenes (every glTF scene: no planes, boxes or ellipsoids, all
+// lights triangles) run the resumable kernel's TO instance, which carries no
+// shape candidate across its loop.  RT_TRIONLY=0 disables it (tests, tuning).
+bool path_trionly(const rt_scene* s) {
+    if (const char* e = std::getenv("RT_TRIONLY")) {
+        if (e[0] == '0') return false;
+    }
+    const DevScene& d = s->dev;
+    return d.n_planes == 0 && d.boxes.n_prims == 0 && d.ells.n_prims == 0 && d.lboxes.n_prims == 0 &&
+           d.lells.n_prims == 0;
+}
+
 // Workspace of one path-kernel launch: persistent grid size, then the spill,
 // ring and chunk-partial buffers sized for it (all grow-only, scene-owned).
 int prepare_path(rt_scene* s, const KParams& k, bool stats, bool hits, PathWork& W) {
@@ -283,7 +295,8 @@ int prepare_path(rt_scene* s, const KParams& k, bool stats, bool hits, PathWork&
     std::memset(&W, 0, sizeof(W));
     W.waves = path_waves(s);
     W.resume = path_resume(s);
-    HIP_TRY(path_grid(stats, hits, W.waves, W.resume, (uint32_t)n_units, &W.grid));
+    W.trionly = path_trionly(s);
+    HIP_TRY(path_grid(stats, hits, W.waves, W.resume, W.trionly, (uint32_t)n_units, &W.grid));
     int rc;
     if ((rc = ensure_spill(s, (uint64_t)W.grid * 64)) || (rc = ensure_part(s, k))) return rc;
     if (!s->queue) HIP_TRY(hipMalloc(&s->queue, kQueueWords * sizeof(uint32_t)));
