@@ -275,16 +275,20 @@ bool path_resume(const rt_scene* s) {
     return s->info.bvh_nodes[2] > kDeepSceneNodes;
 }
 
-// Triangle-only scenes (every glTF scene: no planes, boxes or ellipsoids, all
-// lights triangles) run the resumable kernel's TO instance, which carries no
-// shape candidate across its loop.  RT_TRIONLY=0 disables it (tests, tuning).
-bool path_trionly(const rt_scene* s) {
-    if (const char* e = std::getenv("RT_TRIONLY")) {
-        if (e[0] == '0') return false;
+// The scene's primitive kinds: 1 = shapes (planes, boxes, ellipsoids), 2 =
+// triangles, 3 = both (or neither).  One-kind scenes run kernel instances with no
+// code or state for the other kind: triangle-only ones (every glTF scene) the
+// 4-wave resumable kernel without a shape candidate carried across its loop
+// (C3 -6%), shape-only ones (the Cornell box) the fused kernel without triangle
+// traversal.  RT_KINDS=3 forces the general instances (tests, tuning).
+int path_kinds(const rt_scene* s) {
+    if (const char* e = std::getenv("RT_KINDS")) {
+        if (e[0] == '3') return 3;
     }
     const DevScene& d = s->dev;
-    return d.n_planes == 0 && d.boxes.n_prims == 0 && d.ells.n_prims == 0 && d.lboxes.n_prims == 0 &&
-           d.lells.n_prims == 0;
+    const bool shapes = d.n_planes || d.boxes.n_prims || d.ells.n_prims || d.lboxes.n_prims || d.lells.n_prims;
+    const bool tris = d.tris.n_prims || d.ltris.n_prims;
+    return shapes == tris ? 3 : (shapes ? 1 : 2);
 }
 
 // Workspace of one path-kernel launch: persistent grid size, then the spill,
@@ -295,8 +299,8 @@ int prepare_path(rt_scene* s, const KParams& k, bool stats, bool hits, PathWork&
     std::memset(&W, 0, sizeof(W));
     W.waves = path_waves(s);
     W.resume = path_resume(s);
-    W.trionly = path_trionly(s);
-    HIP_TRY(path_grid(stats, hits, W.waves, W.resume, W.trionly, (uint32_t)n_units, &W.grid));
+    W.kinds = path_kinds(s);
+    HIP_TRY(path_grid(stats, hits, W.waves, W.resume, W.kinds, (uint32_t)n_units, &W.grid));
     int rc;
     if ((rc = ensure_spill(s, (uint64_t)W.grid * 64)) || (rc = ensure_part(s, k))) return rc;
     if (!s->queue) HIP_TRY(hipMalloc(&s->queue, kQueueWords * sizeof(uint32_t)));

@@ -57,7 +57,7 @@ struct PathWork {
     KParams* d_params;        // frame constants slot, staged by launch_path
     uint32_t waves;       // register budget of the kernel instance: 3 or 4 waves/SIMD
     bool resume;          // resumable triangle traversal (path_kernel RES)
-    bool trionly;         // triangles only (path_kernel TO; the 4-wave resumable kernel)
+    int kinds;            // the scene's primitive kinds, kShapes 1 | kTris 2 (path_kernel KM)
     uint32_t grid;        // persistent waves (path_grid)
     uint32_t* queue;      // wave-tile counter, zeroed by launch_path
     double* ring;         // [grid][kRing=8][64][3] finished-path radiance
@@ -72,7 +72,7 @@ constexpr uint32_t kRingRows = RT_RING_ROWS;   // render.hip kRing (power of two
 constexpr uint64_t kDeepSceneNodes = 4096;  // BVH nodes above which the 4-wave kernel runs
 constexpr size_t kQueueWords = 16;  // wave-tile counter (word 0), padded to a 64-B line
 
-hipError_t path_grid(bool stats, bool hits, uint32_t waves, bool resume, bool trionly, uint32_t n_units,
+hipError_t path_grid(bool stats, bool hits, uint32_t waves, bool resume, int kinds, uint32_t n_units,
                      uint32_t* grid);
 hipError_t launch_path(const DevScene& S, const KParams& P, const PathWork& W, double* out, int32_t* hit_ids,
                        unsigned long long* stats, hipStream_t st);

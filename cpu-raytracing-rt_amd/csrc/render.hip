@@ -100,6 +100,10 @@ RT_D Stack<OPQ> make_stack(uint32_t* s_n, double* s_t, uint32_t wave_tid, uint64
     return k;
 }
 
+// A scene's primitive kinds (host: api.cpp path_kinds): kernel instances for
+// one-kind scenes carry no code or state for the other kind.
+constexpr int kShapes = 1, kTris = 2;
+
 // Best candidate of one query: materialised into a Hit only for the winner.
 struct Cand {
     double t;
@@ -452,15 +456,16 @@ RT_D bool bvh_closest_sel(const DevBvh& B, bool rfast, V3 o, V3 d, const Rcp3& r
 }
 
 // Materialise the winning candidate: model-space normals + their rotation, or
-// (world = true) the final world normals.  TO: a triangle-only scene (the
-// candidate is a triangle).
-template <bool TO = false>
+// (world = true) the final world normals.  KM: the scene's primitive kinds
+// (kShapes | kTris, below), so a one-kind scene's instance has no code for the
+// other kind.
+template <int KM = 3>
 RT_D Hit materialise(const DevScene& S, const Cand& c, V3 o, V3 d, Quat& rot, uint32_t& mat, int32_t& gid,
                      bool& world) {
     Hit h;
     h.t = c.t;
     world = false;
-    if (TO || c.kind == 3) {  // Triangle::intersection tail (triangle.rs:71-79), DONT_ROTATE
+    if (KM == kTris || (KM & kTris && c.kind == 3)) {  // Triangle::intersection tail (triangle.rs:71-79), DONT_ROTATE
         const DevBvh& B = S.tris;
         const DevTriCold& tc = B.tri_cold[c.prim];
         V3 n = load3(tc.ng), na = load3(tc.na), nb = load3(tc.nb), nc = load3(tc.nc);
@@ -664,7 +669,7 @@ RT_D void take_tri(Cand& best, bool valid, double t, double u, double v, uint32_
         best.valid = true; best.t = t; best.prim = p; best.u = u; best.v = v; best.aux = 0; best.kind = 3;
     }
 }
-template <bool ST, bool TO = false>
+template <bool ST, int KM = 3>
 RT_D bool intersect_tail(const DevScene& S, const Cand& best, V3 o, V3 d, Cnt<ST>& C, Hit& out, uint32_t& mat,
                          int32_t& gid) {
     if (!best.valid) return false;
@@ -677,25 +682,27 @@ RT_D bool intersect_tail(const DevScene& S, const Cand& best, V3 o, V3 d, Cnt<ST
     const unsigned long long ph = PH_T();
     Quat rot;
     bool world;
-    Hit h = materialise<TO>(S, best, o, d, rot, mat, gid, world);
+    Hit h = materialise<KM>(S, best, o, d, rot, mat, gid, world);
     out = world ? h : rotated(h, rot);
     PH_ADD(kPhMaterialise, ph);
     C.shaded();
     return true;
 }
-template <bool ST, class Stk, bool SLT = false>
+template <bool ST, class Stk, bool SLT = false, int KM = 3>
 RT_D bool scene_intersect(const DevScene& S, V3 o, V3 d, Stk& stk, Cnt<ST>& C, Hit& out, uint32_t& mat,
                           int32_t& gid, bool pend = false, double* impact = nullptr) {
     const Rcp3 rc = make_rcp3(d);
     const bool rfast = ray_fast(o, rc);
     Cand best;
     shapes_closest<ST, false, Stk, SLT>(S, o, d, rc, rfast, stk, C, best, pend, impact);
-    const unsigned long long ph = PH_T();
-    double t, u = 0.0, v = 0.0; uint32_t p = 0, aux = 0;
-    const bool th = bvh_closest_sel<3, ST>(S.tris, rfast, o, d, rc, stk, C, t, u, v, p, aux);
-    take_tri(best, th, t, u, v, p);
-    PH_ADD(kPhTris, ph);
-    return intersect_tail<ST>(S, best, o, d, C, out, mat, gid);
+    if (KM & kTris) {
+        const unsigned long long ph = PH_T();
+        double t, u = 0.0, v = 0.0; uint32_t p = 0, aux = 0;
+        const bool th = bvh_closest_sel<3, ST>(S.tris, rfast, o, d, rc, stk, C, t, u, v, p, aux);
+        take_tri(best, th, t, u, v, p);
+        PH_ADD(kPhTris, ph);
+    }
+    return intersect_tail<ST, KM>(S, best, o, d, C, out, mat, gid);
 }
 
 // ---------------------------------------------------------- light pdf ----
@@ -823,25 +830,25 @@ RT_D void bvh_all(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool rfast, Stk& 
     }
 }
 
-// intersect_lights (intersections.rs:87-91): boxes, ellipsoids, triangles (TO:
-// a triangle-only scene, whose light box and ellipsoid BVHs are empty)
-template <bool ST, class Stk, bool TO = false>
+// intersect_lights (intersections.rs:87-91): boxes, ellipsoids, triangles (KM:
+// the scene's primitive kinds; the light BVHs of an absent kind are empty)
+template <bool ST, class Stk, int KM = 3>
 RT_D double lights_impact(const DevScene& S, V3 o, V3 d, Stk& stk, Cnt<ST>& C, uint32_t& nhits) {
     double impact = 0.0;
     const Rcp3 rc = make_rcp3(d);
     const bool rfast = ray_fast(o, rc);
-    if (!TO) {
+    if (KM & kShapes) {
         bvh_all<1, ST>(S.lboxes, o, d, rc, rfast, stk, C, impact, nhits);
         bvh_all<2, ST>(S.lells, o, d, rc, rfast, stk, C, impact, nhits);
     }
-    bvh_all<3, ST>(S.ltris, o, d, rc, rfast, stk, C, impact, nhits);
+    if (KM & kTris) bvh_all<3, ST>(S.ltris, o, d, rc, rfast, stk, C, impact, nhits);
     return impact;
 }
-template <bool ST, class Stk, bool TO = false>
+template <bool ST, class Stk, int KM = 3>
 RT_D double light_pdf(const DevScene& S, V3 pos, V3 dir, Stk& stk, Cnt<ST>& C) {  // ray_sampler.rs:132-139
     C.lq();
     uint32_t nh = 0;
-    double impact = lights_impact<ST, Stk, TO>(S, pos + dir * kEpsilon, dir, stk, C, nh);
+    double impact = lights_impact<ST, Stk, KM>(S, pos + dir * kEpsilon, dir, stk, C, nh);
     const uint32_t nl = S.n_lights;  // x / 1 == x exactly: skip the division sequence for one light
     return nl == 1u ? impact : impact / (double)nl;
 }
@@ -883,7 +890,7 @@ RT_D V3 uniform_on_box(V3 s, uint64_t A, uint64_t B, uint64_t C, Rng& r, const S
     else p = v3(u1, u2, sign);
     return mul(p, s);
 }
-template <bool TO = false>
+template <int KM = 3>
 RT_D V3 light_point(const DevScene& S, uint64_t A, uint64_t B, uint64_t C, Rng& r,
                     const Scales& sc) {  // ray_sampler.rs:101-129
     // a one-element range needs no draw (the result is 0 either way; oracle.c gen_range_usize)
@@ -893,13 +900,14 @@ RT_D V3 light_point(const DevScene& S, uint64_t A, uint64_t B, uint64_t C, Rng& 
         rng_top_up(r);
         index = gen_index(r, nl, S.light_zone);
     }
+    constexpr bool TO = KM == kTris;
     const uint32_t nb = TO ? 0u : S.lboxes.n_prims, ne = TO ? 0u : S.lells.n_prims;
     V3 world;
     if (!TO && index < nb) {
         const DevShape l = S.lboxes.shapes[index];
         const Quat q = load_quat(l.rot);
         world = rotate_fast(q, is_identity(q), uniform_on_box(load3(l.shape), A, B, C, r, sc)) + load3(l.pos);
-    } else if (!TO && index < (uint64_t)nb + ne) {
+    } else if (!TO && (KM == kShapes || index < (uint64_t)nb + ne)) {
         const DevShape l = S.lells.shapes[index - nb];
         const Quat q = load_quat(l.rot);
         world = rotate_fast(q, is_identity(q), mul(nrm(cube_point(A, B, C)), load3(l.shape))) + load3(l.pos);
@@ -955,14 +963,14 @@ struct SegQuery {
 
 // raytrace_impl's `intersect` call (raytrace.rs:13), first part: planes,
 // boxes and ellipsoids to completion, then the triangle traversal is set up.
-// TO: a triangle-only scene: no shapes to test, and the candidate is the
-// triangle traversal's alone (q.best is not carried across the loop)
-template <bool ST, bool TO = false, class Stk>
+// KM == kTris (a triangle-only scene): no shapes to test, and the candidate is
+// the triangle traversal's alone (q.best is not carried across the loop)
+template <bool ST, int KM = 3, class Stk>
 RT_D void segment_begin(const DevScene& S, const PathState& ps, Stk& stk, Cnt<ST>& C, SegQuery& q) {
     C.segment();
     q.rc = make_rcp3(ps.d);
     const bool rfast = ray_fast(ps.o, q.rc);
-    if (!TO) shapes_closest<ST, true>(S, ps.o, ps.d, q.rc, rfast, stk, C, q.best);
+    if (KM != kTris) shapes_closest<ST, true>(S, ps.o, ps.d, q.rc, rfast, stk, C, q.best);
     q.fast = S.tris.fast && rfast;
     trav_init<2, ST>(S.tris, ps.o, ps.d, q.rc, q.fast, stk, C, q.T);
 }
@@ -971,7 +979,7 @@ RT_D void segment_begin(const DevScene& S, const PathState& ps, Stk& stk, Cnt<ST
 // the closest-hit result on.  Returns true when the path continues with the
 // updated ray.  `last`: this is the path's last segment (raytrace_impl with
 // left == 1).
-template <bool ST, class Stk, bool SLT = false, bool TO = false>
+template <bool ST, class Stk, bool SLT = false, int KM = 3>
 RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, PathState& ps, Rng& rng,
                         Stk& stk, Cnt<ST>& C, bool hit, const Hit& h, uint32_t mat, int32_t gid,
                         int32_t& hit_gid, bool more, bool last) {
@@ -1012,7 +1020,7 @@ RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, P
             degen = fabs(sw.x) <= eps && fabs(sw.y) <= eps && fabs(sw.z) <= eps;
         } else {
             const unsigned long long ph1 = PH_T();
-            sw = light_point<TO>(S, ua, ub, uc, rng, sc) - pos;
+            sw = light_point<KM>(S, ua, ub, uc, rng, sc) - pos;
             PH_ADDW(kPhLightSample, ph1);
         }
         dir = degen ? h.ns : nrm(sw);
@@ -1033,7 +1041,7 @@ RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, P
         double lp = 0.0;
         if (!empty) {
             const unsigned long long ph2 = PH_T();
-            lp = light_pdf<ST, Stk, TO>(S, pos, dir, stk, C);
+            lp = light_pdf<ST, Stk, KM>(S, pos, dir, stk, C);
             PH_ADDW(kPhLightPdf, ph2);
         }
         const double cp = cosine_pdf(h.ns, dir);
@@ -1080,30 +1088,30 @@ RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, P
 }
 
 // the resumable form's end of a segment: finish `intersect`, then shade
-template <bool ST, bool TO = false, class Stk>
+template <bool ST, int KM = 3, class Stk>
 RT_D bool segment_end(const DevScene& S, const KParams& P, const Scales& sc, PathState& ps, Rng& rng,
                       Stk& stk, Cnt<ST>& C, SegQuery& q, int32_t& hit_gid) {
     Hit h; uint32_t mat = 0; int32_t gid = 0;
-    if (TO) {  // the candidate is the triangle traversal's (take_tri on an empty best)
+    if (KM == kTris) {  // the candidate is the triangle traversal's (take_tri on an empty best)
         q.best.valid = false; q.best.t = 0.0; q.best.u = q.best.v = 0.0; q.best.prim = 0; q.best.aux = 0;
         q.best.kind = 0;
     }
     take_tri(q.best, q.T.valid, q.T.best, q.T.bu, q.T.bv, q.T.prim);
-    const bool hit = intersect_tail<ST, TO>(S, q.best, ps.o, ps.d, C, h, mat, gid);
+    const bool hit = intersect_tail<ST, KM>(S, q.best, ps.o, ps.d, C, h, mat, gid);
     // (no last-segment shortcut here: it cost the 4-wave resumable kernel's
     // register allocation more than it saved, C3 +1.5%)
-    return segment_shade<ST, Stk, false, TO>(S, P, sc, ps, rng, stk, C, hit, h, mat, gid, hit_gid, false, false);
+    return segment_shade<ST, Stk, false, KM>(S, P, sc, ps, rng, stk, C, hit, h, mat, gid, hit_gid, false, false);
 }
 
 // the fused form: one whole segment (scene_intersect to completion, then shade)
-template <bool ST, class Stk>
+template <bool ST, int KM = 3, class Stk>
 RT_D bool segment(const DevScene& S, const KParams& P, const Scales& sc, PathState& ps, Rng& rng, Stk& stk,
                   Cnt<ST>& C, int32_t& hit_gid, bool more) {
     Hit h; uint32_t mat; int32_t gid;
     C.segment();
     const unsigned long long ph0 = PH_T();
     double impact = 0.0;
-    const bool hit = scene_intersect<ST, Stk, true>(S, ps.o, ps.d, stk, C, h, mat, gid, ps.pend, &impact);
+    const bool hit = scene_intersect<ST, Stk, true, KM>(S, ps.o, ps.d, stk, C, h, mat, gid, ps.pend, &impact);
     if (ps.pend) {  // the previous bounce's Mix pdf and weight (raytrace.rs:26-33, ray_sampler.rs:95-97)
         const uint32_t nl = S.n_lights;
         const double lp = nl == 1u ? impact : impact / (double)nl;
@@ -1112,7 +1120,7 @@ RT_D bool segment(const DevScene& S, const KParams& P, const Scales& sc, PathSta
         ps.pend = false;
     }
     PH_ADDW(kPhIntersect, ph0);
-    return segment_shade<ST, Stk, true>(S, P, sc, ps, rng, stk, C, hit, h, mat, gid, hit_gid, more, !more);
+    return segment_shade<ST, Stk, true, KM>(S, P, sc, ps, rng, stk, C, hit, h, mat, gid, hit_gid, more, !more);
 }
 
 template <bool ST>
@@ -1223,7 +1231,7 @@ RT_D uint32_t unit_of_row(const uint32_t* uq, uint32_t uq_back, uint32_t row) {
     return i % kUQ;
 }
 
-template <bool ST, bool HIT, int WAVES, bool RES, bool TO = false>
+template <bool ST, bool HIT, int WAVES, bool RES, int KM = 3>
 __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams Pv,
                                                      const DevScene* __restrict__ Sg,
                                                      const KParams* __restrict__ Pg, double* __restrict__ out,
@@ -1370,7 +1378,7 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
             // lanes between segments (new paths, continued paths) start their query
             const unsigned long long ph_b = PH_T();
             if (busy && !inq && b < depth) {
-                segment_begin<ST, TO>(S, ps, stk, C, q);
+                segment_begin<ST, KM>(S, ps, stk, C, q);
                 inq = true;
             }
             PH_ADDW(kPhIntersect, ph_b);
@@ -1397,7 +1405,7 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
                 if (inq) {
                     int32_t g;
                     const unsigned long long ph_s = PH_T();
-                    cont = segment_end<ST, TO>(S, P, sc, ps, rng, stk, C, q, g);
+                    cont = segment_end<ST, KM>(S, P, sc, ps, rng, stk, C, q, g);
                     PH_ADDW(kPhSegment, ph_s);
                     if (HIT) hit_ids[(pixel * P.spp + s) * depth + b] = g;
                     ++b;
@@ -1411,7 +1419,7 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
             if (b < depth) {
                 int32_t g;
                 const unsigned long long ph_s = PH_T();
-                cont = segment<ST>(S, P, sc, ps, rng, stk, C, g, b + 1 < depth);
+                cont = segment<ST, KM>(S, P, sc, ps, rng, stk, C, g, b + 1 < depth);
                 PH_ADDW(kPhSegment, ph_s);
                 if (HIT) hit_ids[(pixel * P.spp + s) * depth + b] = g;
                 ++b;
@@ -1608,34 +1616,37 @@ __global__ void fp64_probe_kernel(const double* a, const double* b, double* out,
 namespace {
 using PathFn = void (*)(DevScene, KParams, const DevScene*, const KParams*, double*, double*, int32_t*,
                         unsigned long long*, uint32_t*, double*, uint32_t*, double*);
-// trionly: the 4-wave resumable kernel has a triangle-only instance (path_kernel TO)
+// kinds (kShapes | kTris): one-kind instances of the two kernels the host picks
+// by default — the 4-wave resumable kernel for triangle-only scenes (every glTF
+// scene) and the 3-wave fused kernel for shape-only scenes (the Cornell box)
 template <bool ST, bool HIT>
-PathFn path_fn_r(uint32_t waves, bool resume, bool trionly) {
-#ifdef RT_ONLY_C2  // experiment builds (tools/variants.py): only the C2 instance, 4x faster to compile
-    (void)waves; (void)resume; (void)trionly;
-    return path_kernel<ST, HIT, 3, false>;
+PathFn path_fn_r(uint32_t waves, bool resume, int kinds) {
+#ifdef RT_ONLY_C2  // experiment builds (tools/variants.py): only the C2 instances, 4x faster to compile
+    (void)waves; (void)resume;
+    return kinds == kShapes ? path_kernel<ST, HIT, 3, false, kShapes> : path_kernel<ST, HIT, 3, false>;
 #elif defined(RT_ONLY_C3)  // ... only the C3 instances
     (void)waves; (void)resume;
-    return trionly ? path_kernel<ST, HIT, 4, true, true> : path_kernel<ST, HIT, 4, true>;
+    return kinds == kTris ? path_kernel<ST, HIT, 4, true, kTris> : path_kernel<ST, HIT, 4, true>;
 #else
-    if (waves == 4 && resume) return trionly ? path_kernel<ST, HIT, 4, true, true> : path_kernel<ST, HIT, 4, true>;
+    if (waves == 4 && resume) return kinds == kTris ? path_kernel<ST, HIT, 4, true, kTris> : path_kernel<ST, HIT, 4, true>;
     if (waves == 4) return path_kernel<ST, HIT, 4, false>;
-    return resume ? path_kernel<ST, HIT, 3, true> : path_kernel<ST, HIT, 3, false>;
+    if (resume) return path_kernel<ST, HIT, 3, true>;
+    return kinds == kShapes ? path_kernel<ST, HIT, 3, false, kShapes> : path_kernel<ST, HIT, 3, false>;
 #endif
 }
-PathFn path_fn(bool stats, bool hits, uint32_t waves, bool resume, bool trionly) {
-    if (stats) return hits ? path_fn_r<true, true>(waves, resume, trionly) : path_fn_r<true, false>(waves, resume, trionly);
-    return hits ? path_fn_r<false, true>(waves, resume, trionly) : path_fn_r<false, false>(waves, resume, trionly);
+PathFn path_fn(bool stats, bool hits, uint32_t waves, bool resume, int kinds) {
+    if (stats) return hits ? path_fn_r<true, true>(waves, resume, kinds) : path_fn_r<true, false>(waves, resume, kinds);
+    return hits ? path_fn_r<false, true>(waves, resume, kinds) : path_fn_r<false, false>(waves, resume, kinds);
 }
 }  // namespace
 
-hipError_t path_grid(bool stats, bool hits, uint32_t waves, bool resume, bool trionly, uint32_t n_units,
+hipError_t path_grid(bool stats, bool hits, uint32_t waves, bool resume, int kinds, uint32_t n_units,
                      uint32_t* grid) {
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e != hipSuccess) return e;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)path_fn(stats, hits, waves, resume, trionly),
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)path_fn(stats, hits, waves, resume, kinds),
                                                      kWave, 0);
     if (e != hipSuccess) return e;
     const uint64_t g = (uint64_t)std::max(per_cu, 1) * (uint64_t)std::max(cus, 1);
@@ -1656,7 +1667,7 @@ hipError_t launch_path(const DevScene& S, const KParams& P, const PathWork& W, d
     hipLaunchKernelGGL(stage_params_kernel, dim3(1), dim3(1), 0, st, W.d_params, P);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(path_fn(stats != nullptr, hit_ids != nullptr, W.waves, W.resume, W.trionly), dim3(W.grid),
+    hipLaunchKernelGGL(path_fn(stats != nullptr, hit_ids != nullptr, W.waves, W.resume, W.kinds), dim3(W.grid),
                        dim3(kWave), 0, st,
                        S, P, W.d_scene, W.d_params, out, W.part, hit_ids, stats, W.spill_n, W.spill_t, W.queue, W.ring);
     e = hipGetLastError();
