@@ -101,6 +101,23 @@ PMC_PASSES = (
 )
 
 
+DIST_ENV = ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+            "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT",
+            "TORCHELASTIC_RESTART_COUNT", "TORCHELASTIC_MAX_RESTARTS", "TORCHELASTIC_RUN_ID",
+            "TORCHELASTIC_USE_AGENT_STORE", "TORCH_NCCL_ASYNC_ERROR_HANDLING")
+
+
+def child_env(env):
+    """Environment of a PMC child: the parent's, minus the torchrun rendezvous
+    variables, so the child is a standalone one-GPU process on the parent's
+    device and never joins (or blocks) the parent's process group."""
+    out = {k: v for k, v in env.items() if k not in DIST_ENV}
+    local = env.get("LOCAL_RANK")
+    if local is not None and "HIP_VISIBLE_DEVICES" not in env and "CUDA_VISIBLE_DEVICES" not in env:
+        out["HIP_VISIBLE_DEVICES"] = local  # rank 0's own GPU
+    return out
+
+
 def pmc_counters(args, world):
     """Counters of the timed path kernel's launch, from child rocprofv3 --pmc
     passes of this same workload (rank 0's tile share of a world-`world`
@@ -113,6 +130,7 @@ def pmc_counters(args, world):
     if shutil.which("rocprofv3") is None:
         return None, "rocprofv3 not found"
     vals, ns = {}, None
+    env = child_env(os.environ)
     with tempfile.TemporaryDirectory(prefix="rt_pmc_") as td:
         for i, counters in enumerate(PMC_PASSES):
             d = os.path.join(td, f"p{i}")
@@ -120,7 +138,7 @@ def pmc_counters(args, world):
                    sys.executable, os.path.abspath(__file__), "--workload", args.workload, "--steps", "1",
                    "--warmup", "0", "--no-cpu-baseline", "--no-pmc", "--as-rank0-of", str(world)]
             cmd += ["--spp", str(args.spp)] if args.spp else []
-            r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env)
             if r.returncode != 0:
                 return None, f"rocprofv3 --pmc {' '.join(counters)} failed rc={r.returncode}: {r.stderr[-300:]}"
             rows = []
@@ -248,6 +266,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.as_rank0_of:  # a PMC child is a standalone process, whatever its environment says
+        world, rank, local = 1, 0, 0
     pmc, pmc_ns = None, "not collected (--no-pmc)"
     if rank == 0 and not args.no_pmc and not args.as_rank0_of:  # before this process touches the GPU
         pmc, pmc_ns = pmc_counters(args, world)
