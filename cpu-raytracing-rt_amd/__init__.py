@@ -135,7 +135,14 @@ EXPORTS = {
     "rt_probe_fp64": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]),
     "rt_bvh_build": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64), C.c_void_p, C.c_void_p, C.c_void_p,
                                C.POINTER(C.c_uint32)]),
+    "rt_multi_create": (C.c_int, [C.POINTER(rt_scene_desc), C.POINTER(C.c_int), C.c_uint32, C.c_uint32,
+                                  C.POINTER(C.c_void_p)]),
+    "rt_multi_render": (C.c_int, [C.c_void_p, C.POINTER(rt_render_params), C.c_void_p, C.c_void_p,
+                                  C.POINTER(rt_stats)]),
+    "rt_multi_scene": (C.c_void_p, [C.c_void_p, C.c_uint32]),
+    "rt_multi_destroy": (None, [C.c_void_p]),
 }
+RT_MULTI_PEER = 0x1
 
 _lib = None
 
@@ -424,6 +431,45 @@ class Scene:
         out = np.zeros(n, np.uint64)
         _check(lib().rt_read_raw_stats(self._h, out.ctypes.data_as(C.c_void_p), n))
         return out
+
+
+class MultiScene:
+    """generate_image over several GPUs of one process (rt_multi_*): one scene
+    replica per listed device (BVHs built once), the frame's tiles dealt
+    round-robin, one gather to devices[0] (RCCL ncclGather, or peer copies with
+    peer=True, which also allows a device listed twice)."""
+
+    def __init__(self, desc: SceneDesc, devices, peer: bool = False):
+        self.desc = desc
+        self.devices = [int(d) for d in devices]
+        d, keep = desc.to_c()
+        devs = (C.c_int * len(self.devices))(*self.devices)
+        h = C.c_void_p()
+        _check(lib().rt_multi_create(C.byref(d), devs, len(self.devices), RT_MULTI_PEER if peer else 0,
+                                     C.byref(h)))
+        self._h = h
+        del keep
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().rt_multi_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def generate_image(self, params: RenderParams, ppm_bytes: bool = False, stats: bool = False):
+        """(mean radiance [H, W, 3] f64, PPM payload [H, W, 3] u8 or None, stats dict)."""
+        p = params.replace(flags=params.flags | (RT_FLAG_STATS if stats else 0)).to_c()
+        img = np.zeros((params.height, params.width, 3), np.float64)
+        byts = np.zeros((params.height, params.width, 3), np.uint8) if ppm_bytes else None
+        st = rt_stats()
+        _check(lib().rt_multi_render(self._h, C.byref(p), img.ctypes.data_as(C.c_void_p),
+                                     None if byts is None else byts.ctypes.data_as(C.c_void_p), C.byref(st)))
+        return img, byts, st.as_dict()
 
 
 def tile_layout(width: int, height: int, world: int):

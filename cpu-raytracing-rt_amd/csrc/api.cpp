@@ -366,10 +366,25 @@ int rt_scene_create(const rt_scene_desc* desc, rt_scene** out) {
     if (!desc || !out) return set_error(RT_ERR_INVALID, "desc/out is NULL");
     *out = nullptr;
     HostScene hs;
-    std::string err = build_scene(*desc, hs);
+    const int rc = rt::scene_build_host(*desc, hs);
+    return rc ? rc : rt::scene_upload(hs, out);
+}
+
+}  // extern "C"
+
+namespace rt {
+
+int scene_build_host(const rt_scene_desc& desc, HostScene& hs) {
+    std::string err = build_scene(desc, hs);
     if (!err.empty()) return set_error(RT_ERR_INVALID, err);
     for (int k = 0; k < 6; ++k)  // traversal stack words carry node indices in 30 bits (render.hip child_word)
         if (hs.bvh[k].nodes.size() >= (1u << 30)) return set_error(RT_ERR_INVALID, "BVH exceeds 2^30 nodes");
+    return RT_OK;
+}
+
+// Scene::new's device side: the flattened scene on the CURRENT HIP device.
+int scene_upload(const HostScene& hs, rt_scene** out) {
+    *out = nullptr;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
         return set_error(RT_ERR_DEVICE, "no HIP device visible (the hot path has no CPU fallback)");
@@ -440,6 +455,10 @@ int rt_scene_create(const rt_scene_desc* desc, rt_scene** out) {
     *out = owner.release();
     return RT_OK;
 }
+
+}  // namespace rt
+
+extern "C" {
 
 void rt_scene_destroy(rt_scene* s) { free_scene(s); }
 

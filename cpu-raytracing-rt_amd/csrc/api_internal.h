@@ -9,6 +9,13 @@ namespace rt {
 
 int set_error(int code, const std::string& msg);  // records rt_last_error, returns code
 
+struct HostScene;
+// rt_scene_create in two halves (api.cpp): the host build (six BVHs, flattened
+// records) and the upload of that build to the current HIP device, so a
+// multi-GPU frame (multi.cpp) builds once and uploads one replica per device.
+int scene_build_host(const rt_scene_desc& desc, HostScene& hs);
+int scene_upload(const HostScene& hs, rt_scene** out);
+
 }  // namespace rt
 
 // Host-side parse result of the input surfaces (custom text / glTF).

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RT_API_VERSION 2
+#define RT_API_VERSION 3
 
 typedef enum rt_error {
     RT_OK = 0,
@@ -239,6 +239,41 @@ int rt_unpack_tiles_bytes_async(const rt_render_params* params, uint32_t world,
 /* Device tonemap + gamma + PPM bytes of a mean-radiance image already in HBM
    ([n_pixels][3] f64 -> [n_pixels][3] u8). */
 int rt_tonemap_bytes_async(const double* d_rgb, uint64_t n_pixels, uint8_t* d_bytes, void* hip_stream);
+
+/* ======================= one process, several GPUs ======================== */
+/* generate_image (src/main.rs:85-114) over several GPUs of one node, driven
+   from ONE host thread exactly like rt_render (the Rust `main`, main.rs:73,
+   keeps its single call per frame):
+    - rt_multi_create builds the six BVHs once on the host (scene.rs:180-223,
+      bvh.rs:12-17) and uploads one scene replica per listed device;
+    - rt_multi_render deals the frame's 16x16 tiles round-robin (tile t ->
+      device index t % n, the rt_render_tiles_async partition), renders every
+      share on its own device and stream, makes ONE gather of the packed tiles
+      to devices[0] (an RCCL ncclGather over xGMI; peer copies with
+      RT_MULTI_PEER), then unpacks on devices[0] and copies the image to the
+      host once.
+   The image is bit-identical to rt_render's for any device count (the RNG is
+   keyed by the global pixel and sample, the chunking by the frame alone).
+   out_mean_rgb: NULL or caller-owned [H][W][3] f64 (main.rs:104 before the
+   tonemap); out_ppm_bytes: NULL or caller-owned [H][W][3] u8, the P6 payload
+   of correct_gamma(aces_tonemap(.)) made on the device (as
+   rt_unpack_tiles_bytes_async); at least one is required.  opt_stats: work
+   counters summed over the devices (RT_FLAG_STATS), kernel_ms = the slowest
+   device's render, total_ms = the call's wall time.
+   RCCL is loaded at rt_multi_create (dlopen of librccl.so.1); without it, or
+   with a device listed twice, RT_MULTI_PEER is required. */
+#define RT_MULTI_PEER 0x1u  /* gather with hipMemcpyPeerAsync instead of RCCL;
+                               allows a device listed more than once (several
+                               replicas on one GPU: a rehearsal of the N-way
+                               partition on a one-GPU machine) */
+typedef struct rt_multi rt_multi;
+int  rt_multi_create(const rt_scene_desc* desc, const int* devices, uint32_t n_devices, uint32_t flags,
+                     rt_multi** out);
+int  rt_multi_render(rt_multi* m, const rt_render_params* params, double* out_mean_rgb,
+                     uint8_t* out_ppm_bytes, rt_stats* opt_stats);
+/* The replica on device index i (0 <= i < n) for per-device queries; owned by m. */
+rt_scene* rt_multi_scene(rt_multi* m, uint32_t index);
+void rt_multi_destroy(rt_multi* m);
 
 /* ======================= ray queries ====================================== */
 /* Closest hit for a batch of world rays [n][6] = (origin, dir) — replaces

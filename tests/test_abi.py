@@ -30,7 +30,7 @@ def test_header_symbols_exported(rt):
 
 
 def test_version_and_errors(rt):
-    assert rt.lib().rt_api_version() == 2
+    assert rt.lib().rt_api_version() == 3
     with pytest.raises(rt.RtError) as e:
         rt.parse_scene("NEW_PRIMITIVE\nBOX 1 2\n")
     assert e.value.code == -4
@@ -43,6 +43,28 @@ def test_no_cpu_fallback(rt, scene_text):
     with pytest.raises(rt.RtError) as e:
         rt.Scene(desc)
     assert e.value.code == -2 and "no HIP device" in str(e.value)
+    for peer in (False, True):  # the multi-GPU entry refuses the same way
+        with pytest.raises(rt.RtError) as e:
+            rt.MultiScene(desc, [0, 1], peer=peer)
+        assert e.value.code == -2 and "no HIP device" in str(e.value)
+
+
+def test_multi_argument_errors(rt, scene_text):
+    """rt_multi_* reject bad arguments before touching a device."""
+    import ctypes as C
+    L = rt.lib()
+    desc, params = rt.parse_scene(scene_text("cornell.txt"))
+    d, keep = desc.to_c()
+    h = C.c_void_p()
+    devs = (C.c_int * 1)(0)
+    assert L.rt_multi_create(C.byref(d), devs, 0, 0, C.byref(h)) == -1       # no devices
+    assert L.rt_multi_create(C.byref(d), devs, 1, 0x80, C.byref(h)) == -1    # unknown flag
+    assert L.rt_multi_create(None, devs, 1, 0, C.byref(h)) == -1
+    p = params.to_c()
+    assert L.rt_multi_render(None, C.byref(p), None, None, None) == -1
+    assert L.rt_multi_scene(None, 0) is None
+    L.rt_multi_destroy(None)  # no-op
+    del keep
 
 
 # ------------------------------------------------------------- parser ----

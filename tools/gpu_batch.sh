@@ -25,6 +25,11 @@ for s in $STEPS; do
   case $s in
     tests) run pytest_gpu 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread || exit 1 ;;
     bench) run bench_default 900 $B --gpus 1 --steps 20 --warmup 5 || exit 1 ;;
+    multi) run pytest_multi 600 python3 -u -m pytest tests/test_gpu_multi.py -m gpu -x -v --timeout 300 \
+             --timeout-method thread || exit 1 ;;
+    dist2) # the N=2 bench path (PMC children, tile shares, one gather, max-over-ranks) as a gloo rehearsal
+      run bench_dist2 900 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --dist-backend gloo || exit 1 ;;
     c2)    run bench_c2 600 $B --workload C2 --steps 3 --warmup 1 || exit 1 ;;
     c3)    run bench_c3 600 $B --workload C3 --steps 3 --warmup 1 || exit 1 ;;
     c5)    run bench_c5 900 $B --workload C5 --steps 2 --warmup 1 || exit 1 ;;
