@@ -41,7 +41,7 @@ constexpr int kPhaseWord0 = 16;   // RT_PHASES builds: region cycles + loop coun
 // rows across wave-tiles, so short ones cost no drain), capped at spp and
 // kMaxChunks, then trimmed so no chunk is empty.
 constexpr uint64_t kChunkLanes = 32000000;
-constexpr uint32_t kMinChunkSpp = 16;
+constexpr uint32_t kMinChunkSpp = 8;
 constexpr uint32_t kMaxChunks = 64;
 inline void sample_chunks(uint32_t W, uint32_t H, uint32_t spp, uint32_t& chunks, uint32_t& chunk_spp) {
     const uint64_t px = (uint64_t)W * H;

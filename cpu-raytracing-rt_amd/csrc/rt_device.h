@@ -510,13 +510,26 @@ RT_D V3 ell_normal(const Radii& R, V3 o, V3 d, double t) {  // ellipsoid.rs:26,2
 
 // Triangle::intersection (triangle.rs:49-80) up to (u, v, t); normals later.
 RT_D bool tri_uvt(const DevTri& tr, V3 o, V3 d, double& u, double& v, double& t) {
+#ifndef RT_TRI_LAZY  // ablation build: per-field loads
+    // The whole record in one batch of 16-B loads; the asm keeps `a` from being
+    // loaded only after the determinant and its early exit, which exposed a second
+    // memory round trip per test (C3 -1.3%, C5 -1.4% at reduced spp,
+    // profiles/r02/variants/variants_tripre_*.log).
+    const double2* tw = (const double2*)&tr;
+    const double2 w0 = tw[0], w1 = tw[1], w2 = tw[2], w3 = tw[3], w4 = tw[4];
+    asm volatile("" ::"v"(w0.x), "v"(w0.y), "v"(w1.x));
+    const V3 ta = v3(w0.x, w0.y, w1.x);
+    V3 m0 = v3(w1.y, w2.x, w2.y), m1 = v3(w3.x, w3.y, w4.x), m2 = -d;
+#else
+    const V3 ta = load3(tr.a);
     V3 m0 = load3(tr.ba), m1 = load3(tr.ca), m2 = -d;
+#endif
     double det = m0.x * (m1.y * m2.z - m2.y * m1.z) - m1.x * (m0.y * m2.z - m2.y * m0.z) +
                  m2.x * (m0.y * m1.z - m1.y * m0.z);
     if (fabs(det) < 1e-11) return false;
     auto dv = [&](V3 c) { return c / det; };
     V3 x0 = dv(cross(m1, m2)), x1 = dv(cross(m2, m0)), x2 = dv(cross(m0, m1));
-    V3 w = o - load3(tr.a);
+    V3 w = o - ta;
     double uu = dot(x0, w), vv = dot(x1, w), tt = dot(x2, w);
     if (uu < 0.0 || vv < 0.0 || 1.0 < uu + vv || tt < 0.0) return false;
     u = uu; v = vv; t = tt;

@@ -71,6 +71,9 @@ for s in $STEPS; do
       w=C${s#var}
       run variants_$w 900 python3 tools/variants.py $w ${VAR_SPP:-64} ${VARIANTS:-cpu-raytracing-rt_amd/build*/librt_amd.so} \
         || exit 1 ;;
+    share2) run share_C2 600 python3 tools/share_scaling.py C2 256 1 8 || exit 1 ;;
+    var5)  run variants_C5 900 python3 tools/variants.py C5 ${VAR_SPP5:-16} \
+             ${VARIANTS:-cpu-raytracing-rt_amd/build*/librt_amd.so} || exit 1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
