@@ -509,31 +509,38 @@ RT_D V3 ell_normal(const Radii& R, V3 o, V3 d, double t) {  // ellipsoid.rs:26,2
 }
 
 // Triangle::intersection (triangle.rs:49-80) up to (u, v, t); normals later.
+// TriRec: the hot record in registers (a, ba, ca).
+struct TriRec { V3 a, ba, ca; };
+RT_D TriRec load_tri(const DevTri& tr) {  // one batch of 16-B loads
+    const double2* tw = (const double2*)&tr;
+    const double2 w0 = tw[0], w1 = tw[1], w2 = tw[2], w3 = tw[3], w4 = tw[4];
+    return TriRec{v3(w0.x, w0.y, w1.x), v3(w1.y, w2.x, w2.y), v3(w3.x, w3.y, w4.x)};
+}
+RT_D bool tri_uvt_r(const TriRec& r, V3 o, V3 d, double& u, double& v, double& t) {
+    V3 m0 = r.ba, m1 = r.ca, m2 = -d;
+    double det = m0.x * (m1.y * m2.z - m2.y * m1.z) - m1.x * (m0.y * m2.z - m2.y * m0.z) +
+                 m2.x * (m0.y * m1.z - m1.y * m0.z);
+    if (fabs(det) < 1e-11) return false;
+    auto dv = [&](V3 c) { return c / det; };
+    V3 x0 = dv(cross(m1, m2)), x1 = dv(cross(m2, m0)), x2 = dv(cross(m0, m1));
+    V3 w = o - r.a;
+    double uu = dot(x0, w), vv = dot(x1, w), tt = dot(x2, w);
+    if (uu < 0.0 || vv < 0.0 || 1.0 < uu + vv || tt < 0.0) return false;
+    u = uu; v = vv; t = tt;
+    return true;
+}
 RT_D bool tri_uvt(const DevTri& tr, V3 o, V3 d, double& u, double& v, double& t) {
 #ifndef RT_TRI_LAZY  // ablation build: per-field loads
     // The whole record in one batch of 16-B loads; the asm keeps `a` from being
     // loaded only after the determinant and its early exit, which exposed a second
     // memory round trip per test (C3 -1.3%, C5 -1.4% at reduced spp,
     // profiles/r02/variants/variants_tripre_*.log).
-    const double2* tw = (const double2*)&tr;
-    const double2 w0 = tw[0], w1 = tw[1], w2 = tw[2], w3 = tw[3], w4 = tw[4];
-    asm volatile("" ::"v"(w0.x), "v"(w0.y), "v"(w1.x));
-    const V3 ta = v3(w0.x, w0.y, w1.x);
-    V3 m0 = v3(w1.y, w2.x, w2.y), m1 = v3(w3.x, w3.y, w4.x), m2 = -d;
+    const TriRec r = load_tri(tr);
+    asm volatile("" ::"v"(r.a.x), "v"(r.a.y), "v"(r.a.z));
+    return tri_uvt_r(r, o, d, u, v, t);
 #else
-    const V3 ta = load3(tr.a);
-    V3 m0 = load3(tr.ba), m1 = load3(tr.ca), m2 = -d;
+    return tri_uvt_r(TriRec{load3(tr.a), load3(tr.ba), load3(tr.ca)}, o, d, u, v, t);
 #endif
-    double det = m0.x * (m1.y * m2.z - m2.y * m1.z) - m1.x * (m0.y * m2.z - m2.y * m0.z) +
-                 m2.x * (m0.y * m1.z - m1.y * m0.z);
-    if (fabs(det) < 1e-11) return false;
-    auto dv = [&](V3 c) { return c / det; };
-    V3 x0 = dv(cross(m1, m2)), x1 = dv(cross(m2, m0)), x2 = dv(cross(m0, m1));
-    V3 w = o - ta;
-    double uu = dot(x0, w), vv = dot(x1, w), tt = dot(x2, w);
-    if (uu < 0.0 || vv < 0.0 || 1.0 < uu + vv || tt < 0.0) return false;
-    u = uu; v = vv; t = tt;
-    return true;
 }
 
 // Intersection (intersections.rs:10-16)

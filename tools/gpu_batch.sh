@@ -71,6 +71,11 @@ for s in $STEPS; do
       w=C${s#var}
       run variants_$w 900 python3 tools/variants.py $w ${VAR_SPP:-64} ${VARIANTS:-cpu-raytracing-rt_amd/build*/librt_amd.so} \
         || exit 1 ;;
+    wait2|wait3|wait5)  # where wave-time goes: parked on s_waitcnt vs issue stalls vs issuing (one SQ pass)
+      w=C${s#wait}
+      run wait_$w 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU \
+        SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES --output-format csv -d "$OUT/wait_$w" -o run \
+        -- $B --workload $w --steps 1 --warmup 0 --no-cpu-baseline --no-pmc ${WAIT_SPP:+--spp $WAIT_SPP} || exit 1 ;;
     share2) run share_C2 600 python3 tools/share_scaling.py C2 256 1 8 || exit 1 ;;
     var5)  run variants_C5 900 python3 tools/variants.py C5 ${VAR_SPP5:-16} \
              ${VARIANTS:-cpu-raytracing-rt_amd/build*/librt_amd.so} || exit 1 ;;
