@@ -291,9 +291,22 @@ int path_kinds(const rt_scene* s) {
     return shapes == tris ? 3 : (shapes ? 1 : 2);
 }
 
+// Suspend threshold of the resumable traversal (render.h kSuspendCached /
+// kSuspendStreamed): by whether the triangle BVH and its hot records fit the
+// Infinity Cache.  RT_SUSPEND_LANES=<n> forces one (tuning).
+uint32_t path_suspend(const rt_scene* s) {
+    if (const char* e = std::getenv("RT_SUSPEND_LANES")) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v >= 1 && v <= 64) return (uint32_t)v;
+    }
+    const uint64_t bytes = s->info.bvh_nodes[2] * sizeof(DevNode) + s->info.n_triangles * sizeof(DevTri);
+    return bytes > kCacheBytes ? kSuspendStreamed : kSuspendCached;
+}
+
 // Workspace of one path-kernel launch: persistent grid size, then the spill,
 // ring and chunk-partial buffers sized for it (all grow-only, scene-owned).
-int prepare_path(rt_scene* s, const KParams& k, bool stats, bool hits, PathWork& W) {
+int prepare_path(rt_scene* s, KParams& k, bool stats, bool hits, PathWork& W) {
+    k.suspend = path_suspend(s);
     const uint64_t n_units = (uint64_t)k.n_slots * k.chunks * 4;
     if (n_units >= (1ull << 31)) return set_error(RT_ERR_INVALID, "frame too large for one launch");
     std::memset(&W, 0, sizeof(W));

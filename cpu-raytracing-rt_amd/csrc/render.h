@@ -25,7 +25,8 @@ struct KParams {
     // sample chunking (DESIGN.md §4 "work units"): a work unit is (tile slot,
     // chunk of chunk_spp consecutive samples); chunks == 1 writes means directly
     uint32_t chunks, chunk_spp;
-    uint32_t n_slots, _pad;
+    uint32_t n_slots;
+    uint32_t suspend;  // live lanes below which the resumable kernel suspends traversal (api.cpp path_suspend)
 };
 
 // device work counters: paths, segments, aabb, tri, shape, shaded, light queries,
@@ -69,6 +70,14 @@ struct PathWork {
 #define RT_RING_ROWS 8
 #endif
 constexpr uint32_t kRingRows = RT_RING_ROWS;   // render.hip kRing (power of two, <= 64)
+// Suspend threshold of the resumable triangle traversal (path_kernel RES): fewer
+// live lanes than this and the wave lets its waiting lanes shade and start new
+// rays.  A cache-resident BVH (C3, ~40 MB) runs best at 24 (16: +0.3%, 32: +3.7%);
+// one that streams from HBM (C5, ~1.4 GB, past the 256-MiB Infinity Cache) at 40
+// (16: +16.6%, 24: +5.3%, 48: +1.6%; profiles/r02/variants/variants_suspend*.log):
+// there every lane sent back to issue its next ray adds memory-level parallelism.
+constexpr uint32_t kSuspendCached = 24, kSuspendStreamed = 40;
+constexpr uint64_t kCacheBytes = 256ull << 20;  // MI355X Infinity Cache (MALL)
 constexpr uint64_t kDeepSceneNodes = 4096;  // BVH nodes above which the 4-wave kernel runs
 constexpr size_t kQueueWords = 16;  // wave-tile counter (word 0), padded to a 64-B line
 

@@ -34,10 +34,6 @@ constexpr int kShort = kMaxBvhDepthShort;
 #define RT_LEAF_BATCH 16  // lanes waiting at leaves before the wave tests primitives (bvh_closest)
 #endif
 constexpr int kLeafBatch = RT_LEAF_BATCH;
-#ifndef RT_SUSPEND
-#define RT_SUSPEND 16  // live lanes below which the path kernel suspends triangle traversal
-#endif
-constexpr int kSuspend = RT_SUSPEND;
 
 // ---------------------------------------------------------------- stack ---
 // LDS short stack laid out per wave: [wave][slot][lane], so consecutive lanes
@@ -319,6 +315,9 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
         double lt = 0.0, rt2 = 0.0;
         C.aabb(2);
         const NodeBoxes nb = node_boxes(n);
+#ifdef RT_PIN_META
+        asm volatile("" ::"v"(links.x), "v"(links.y), "v"(kids.x), "v"(kids.y), "v"(kids.z), "v"(kids.w));
+#endif
         const bool lh = slab_v<SLAB>(nb.lmn, nb.lmx, o, d, rc, fast, lt);
         const bool rh = slab_v<SLAB>(nb.rmn, nb.rmx, o, d, rc, fast, rt2);
         const double bt = T.best;  // +inf when no hit yet
@@ -1426,14 +1425,14 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
             }
             PH_ADDW(kPhIntersect, ph_b);
             // Triangle traversal, resumable: step while enough lanes are live; once
-            // fewer than kSuspend are, and other lanes wait to shade or to take a new
+            // fewer than P.suspend are, and other lanes wait to shade or to take a new
             // path, suspend the live ones (their stacks and Trav stay put) so the
             // waiting lanes run now and rejoin the traversal with their next rays.
             const unsigned long long ph_t = PH_T();
             for (;;) {
                 const uint64_t lv = __ballot(q.T.live);
                 if (lv == 0) break;
-                if (__popcll(lv) < kSuspend) {
+                if (__popcll(lv) < (int)P.suspend) {
                     const uint32_t win = (base + kRing) * kWave;
                     const bool can_take = next < min(win, open_end * kWave) || (!drained && next < win);
                     if (__ballot((busy && !q.T.live) || (!busy && can_take))) break;

@@ -30,14 +30,18 @@ def sink(rt, orc, scene_text):
     return desc, params, rt.Scene(desc), orc.OracleScene(desc)
 
 
-@pytest.fixture(autouse=True, params=["fused", "resume", "general"])
+@pytest.fixture(autouse=True, params=["fused", "resume", "resume_eager", "general"])
 def segment_form(request, monkeypatch):
     """Every test runs both path-kernel segment forms: fused (whole closest-hit
     query, then shading) and resumable (triangle traversal suspended while few
     lanes are live); the host picks one per scene (RT_RESUME).
+    "resume_eager" suspends whenever any lane waits (RT_SUSPEND_LANES=64, past
+    the HBM-scene threshold the host picks, api.cpp path_suspend).
     "general" is the fused form in its all-kinds instance (RT_KINDS=3) where the
     host would pick a shape-only or triangle-only one (api.cpp path_kinds)."""
-    monkeypatch.setenv("RT_RESUME", "1" if request.param == "resume" else "0")
+    monkeypatch.setenv("RT_RESUME", "1" if request.param.startswith("resume") else "0")
+    if request.param == "resume_eager":
+        monkeypatch.setenv("RT_SUSPEND_LANES", "64")
     if request.param == "general":
         monkeypatch.setenv("RT_KINDS", "3")
     return request.param

@@ -76,6 +76,14 @@ for s in $STEPS; do
       run wait_$w 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU \
         SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES --output-format csv -d "$OUT/wait_$w" -o run \
         -- $B --workload $w --steps 1 --warmup 0 --no-cpu-baseline --no-pmc ${WAIT_SPP:+--spp $WAIT_SPP} || exit 1 ;;
+    l1_2|l1_3|l1_5)  # vector-memory pipe: TA/TD busy and stalls, then L1 (TCP) stalls and latency
+      w=C${s#l1_}
+      run ta_$w 600 rocprofv3 --pmc TA_BUSY_avr TA_DATA_STALLED_BY_TC_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum \
+        GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/ta_$w" -o run \
+        -- $B --workload $w --steps 1 --warmup 0 --no-cpu-baseline --no-pmc ${WAIT_SPP:+--spp $WAIT_SPP} || exit 1
+      run tcp_$w 600 rocprofv3 --pmc TCP_PENDING_STALL_CYCLES_sum TCP_TCR_TCP_STALL_CYCLES_sum TCP_TCP_LATENCY_sum \
+        TCP_TOTAL_CACHE_ACCESSES_sum --output-format csv -d "$OUT/tcp_$w" -o run \
+        -- $B --workload $w --steps 1 --warmup 0 --no-cpu-baseline --no-pmc ${WAIT_SPP:+--spp $WAIT_SPP} || exit 1 ;;
     share2) run share_C2 600 python3 tools/share_scaling.py C2 256 1 8 || exit 1 ;;
     var5)  run variants_C5 900 python3 tools/variants.py C5 ${VAR_SPP5:-16} \
              ${VARIANTS:-cpu-raytracing-rt_amd/build*/librt_amd.so} || exit 1 ;;
