@@ -294,19 +294,34 @@ int path_kinds(const rt_scene* s) {
 // Suspend threshold of the resumable traversal (render.h kSuspendCached /
 // kSuspendStreamed): by whether the triangle BVH and its hot records fit the
 // Infinity Cache.  RT_SUSPEND_LANES=<n> forces one (tuning).
+bool bvh_streamed(const rt_scene* s) {  // the triangle BVH and its hot records exceed the Infinity Cache
+    const uint64_t bytes = s->info.bvh_nodes[2] * sizeof(DevNode) + s->info.n_triangles * sizeof(DevTri);
+    return bytes > kCacheBytes;
+}
 uint32_t path_suspend(const rt_scene* s) {
     if (const char* e = std::getenv("RT_SUSPEND_LANES")) {
         const long v = std::strtol(e, nullptr, 10);
         if (v >= 1 && v <= 64) return (uint32_t)v;
     }
-    const uint64_t bytes = s->info.bvh_nodes[2] * sizeof(DevNode) + s->info.n_triangles * sizeof(DevTri);
-    return bytes > kCacheBytes ? kSuspendStreamed : kSuspendCached;
+    return bvh_streamed(s) ? kSuspendStreamed : kSuspendCached;
+}
+
+// Leaf batch of the resumable traversal (render.hip trav_step: lanes waiting at
+// leaves before the wave tests them), by the same cache criterion as the suspend
+// threshold (render.h kLeafCached / kLeafStreamed).  RT_LEAF_LANES=<n> forces one.
+uint32_t path_leaf_batch(const rt_scene* s) {
+    if (const char* e = std::getenv("RT_LEAF_LANES")) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v >= 1 && v <= 64) return (uint32_t)v;
+    }
+    return bvh_streamed(s) ? kLeafStreamed : kLeafCached;
 }
 
 // Workspace of one path-kernel launch: persistent grid size, then the spill,
 // ring and chunk-partial buffers sized for it (all grow-only, scene-owned).
 int prepare_path(rt_scene* s, KParams& k, bool stats, bool hits, PathWork& W) {
     k.suspend = path_suspend(s);
+    k.leaf_batch = path_leaf_batch(s);
     const uint64_t n_units = (uint64_t)k.n_slots * k.chunks * 4;
     if (n_units >= (1ull << 31)) return set_error(RT_ERR_INVALID, "frame too large for one launch");
     std::memset(&W, 0, sizeof(W));

@@ -26,7 +26,9 @@ struct KParams {
     // chunk of chunk_spp consecutive samples); chunks == 1 writes means directly
     uint32_t chunks, chunk_spp;
     uint32_t n_slots;
-    uint32_t suspend;  // live lanes below which the resumable kernel suspends traversal (api.cpp path_suspend)
+    uint32_t suspend;     // live lanes below which the resumable kernel suspends traversal (api.cpp path_suspend)
+    uint32_t leaf_batch;  // lanes waiting at leaves before the resumable kernel tests them (api.cpp path_suspend)
+    uint32_t _pad;
 };
 
 // device work counters: paths, segments, aabb, tri, shape, shaded, light queries,
@@ -77,6 +79,10 @@ constexpr uint32_t kRingRows = RT_RING_ROWS;   // render.hip kRing (power of two
 // (16: +16.6%, 24: +5.3%, 48: +1.6%; profiles/r02/variants/variants_suspend*.log):
 // there every lane sent back to issue its next ray adds memory-level parallelism.
 constexpr uint32_t kSuspendCached = 24, kSuspendStreamed = 40;
+// Leaf batch of the same kernel (lanes waiting at leaves before the wave tests
+// them): C3 16 -> 32 lanes 236.3 -> 227.1 ms, C5 16 -> 24 lanes 260.3 -> 249.5 ms at
+// 64 spp (profiles/r02/variants/variants_leaflanes*.log).
+constexpr uint32_t kLeafCached = 32, kLeafStreamed = 24;
 constexpr uint64_t kCacheBytes = 256ull << 20;  // MI355X Infinity Cache (MALL)
 constexpr uint64_t kDeepSceneNodes = 4096;  // BVH nodes above which the 4-wave kernel runs
 constexpr size_t kQueueWords = 16;  // wave-tile counter (word 0), padded to a 64-B line

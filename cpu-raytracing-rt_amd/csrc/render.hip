@@ -266,9 +266,9 @@ RT_D void trav_init(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
 // runs with many lanes instead of a few.
 template <int KIND, int SLAB, bool ST, class Stk>
 RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk& S, Cnt<ST>& C, Trav& T,
-                    uint64_t lv) {
+                    uint64_t lv, int leaf_batch = kLeafBatch) {
     const uint64_t at_leaf = __ballot(T.live && T.cnt != 0);
-    const bool do_leaves = at_leaf == lv || __popcll(at_leaf) >= kLeafBatch;
+    const bool do_leaves = at_leaf == lv || __popcll(at_leaf) >= leaf_batch;
     PH_COUNT(kPhTravWave, kPhTravLane);
     if (T.live) PH_LANE(kPhLiveLane);
     bool next = false;  // this lane finished its current node and pops
@@ -1437,7 +1437,7 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
                     const bool can_take = next < min(win, open_end * kWave) || (!drained && next < win);
                     if (__ballot((busy && !q.T.live) || (!busy && can_take))) break;
                 }
-                trav_step<3, 2, ST>(S.tris, ps.o, ps.d, q.rc, q.fast, stk, C, q.T, lv);
+                trav_step<3, 2, ST>(S.tris, ps.o, ps.d, q.rc, q.fast, stk, C, q.T, lv, (int)P.leaf_batch);
             }
             PH_ADD(kPhTris, ph_t);
             // lanes whose query finished shade and end (or continue) their segment

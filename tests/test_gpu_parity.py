@@ -35,13 +35,15 @@ def segment_form(request, monkeypatch):
     """Every test runs both path-kernel segment forms: fused (whole closest-hit
     query, then shading) and resumable (triangle traversal suspended while few
     lanes are live); the host picks one per scene (RT_RESUME).
-    "resume_eager" suspends whenever any lane waits (RT_SUSPEND_LANES=64, past
-    the HBM-scene threshold the host picks, api.cpp path_suspend).
+    "resume_eager" suspends whenever any lane waits and tests every leaf at once
+    (RT_SUSPEND_LANES=64, RT_LEAF_LANES=1: the far ends of the per-scene knobs the
+    host picks, api.cpp path_suspend / path_leaf_batch).
     "general" is the fused form in its all-kinds instance (RT_KINDS=3) where the
     host would pick a shape-only or triangle-only one (api.cpp path_kinds)."""
     monkeypatch.setenv("RT_RESUME", "1" if request.param.startswith("resume") else "0")
     if request.param == "resume_eager":
         monkeypatch.setenv("RT_SUSPEND_LANES", "64")
+        monkeypatch.setenv("RT_LEAF_LANES", "1")
     if request.param == "general":
         monkeypatch.setenv("RT_KINDS", "3")
     return request.param
