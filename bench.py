@@ -49,8 +49,6 @@ WORKLOADS = {
     "C5": ("gltf:hairball", 1920, 1080, 64, None),       # BASELINE configs[4]: 10M-triangle stress scene
 }
 GENERATORS = {"sponza_like": "gen_sponza_like.py", "hairball": "gen_hairball.py"}
-# the oracle restates the reference's O(n log^2 n) builder: skip its CPU leg above this size
-CPU_BASELINE_MAX_TRIS = 2_000_000
 DESCRIPTIONS = {
     "cornell.txt": "Cornell box (scenes/cornell.txt, custom format, 9 primitives, 1 emissive box light)",
     "gltf:sponza_like": "synthetic Sponza-class atrium (scenes/gen_sponza_like.py -> glTF, 263k smooth-normal "
@@ -208,12 +206,32 @@ def valu_roofline(pmc, pmc_ns, kern_s):
     }
 
 
+def cpu_share():
+    """The host cores this process may use: its affinity mask, capped by the cgroup CPU
+    quota when one is set (a GPU box's share of the machine; nproc shows every CPU)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    threads = aff if quota is None else max(1, min(aff, int(quota)))
+    return threads, {"nproc": os.cpu_count(), "affinity": aff, "cgroup_cpus": quota,
+                     "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
+
+
 def cpu_baseline(desc, params, target_s):
-    """Oracle (C restatement, kind "port") on a bounded window of rows at full spp."""
+    """Oracle (C restatement, kind "port") on a bounded window of rows at full spp,
+    on every host core this process may use (rayon uses all cores, main.rs:94)."""
     sys.path.insert(0, os.path.join(HERE, "oracle"))
     import oracle as orc
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    osc = orc.OracleScene(desc)
+    threads, host = cpu_share()
+    print(f"bench: cpu baseline: building the oracle scene on {threads} threads", file=sys.stderr, flush=True)
+    tb = time.perf_counter()
+    osc = orc.OracleScene(desc)  # the restated reference builder: outside the timed leg
+    build_s = time.perf_counter() - tb
     # grow a centred band of rows in small slices until ~target_s of CPU work is
     # done (the box's CPU share varies, so a one-shot calibration over- or
     # under-shoots by several x); the rate is segments / time over all slices
@@ -239,6 +257,8 @@ def cpu_baseline(desc, params, target_s):
         "value": segs / dt / 1e6,
         "unit": "Msamples/s",
         "cores": threads,
+        "host": host,
+        "oracle_build_s": build_s,
         "kind": "port",
         "sample": f"rows {r0}..{r1} of {params.width}x{params.height} at {params.spp} spp "
                   f"({paths} paths, {segs} segments, {dt:.1f} s), recursive raytrace_impl, "
@@ -385,7 +405,8 @@ def main():
                     "measured HBM rate is roofline.hbm (traffic = PMC HBM bytes per launch)",
         })
         out = {
-            "metric": "Msamples/s (rays traced x bounces) at 1920x1080, 256 spp; fraction of HBM roofline",
+            "metric": "Msamples/s (rays traced x bounces) at 1920x1080, 256 spp; fraction of f64 VALU-issue "
+                      "roofline (modelled lower bound; the measured HBM fraction is roofline.hbm)",
             "value": value,
             "unit": "Msamples/s",
             "n_gpus": world,
@@ -410,13 +431,10 @@ def main():
             },
             "roofline": roofline,
             "paths_per_s": frame_paths * args.steps / elapsed,
+            "tuning": scene.tuning(),
             "scene_build_s": build_s,
         }
-        if world == 1 and not args.no_cpu_baseline and len(desc.tri_material) > CPU_BASELINE_MAX_TRIS:
-            out["cpu_baseline"] = None
-            out["cpu_baseline_note"] = (f"skipped: the oracle's restated reference builder (O(n log^2 n)) needs "
-                                        f"minutes for {len(desc.tri_material)} triangles; C3 carries the CPU ratio")
-        elif world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(desc, params, args.cpu_seconds)
             out["speedup_vs_cpu"] = value / out["cpu_baseline"]["value"]
         # the PPM payload of the last frame (outside the timed region): identical for any N

@@ -102,11 +102,23 @@ class rt_scene_info(C.Structure):
                 ("shared_light_mask", C.c_uint32), ("reserved", C.c_uint32)]
 
 
+class rt_tuning(C.Structure):
+    _fields_ = [("waves", C.c_uint32), ("resume", C.c_int32), ("kinds", C.c_uint32),
+                ("suspend_lanes", C.c_uint32), ("leaf_lanes", C.c_uint32), ("chunk_spp", C.c_uint32)]
+
+
+TUNING_AUTO = dict(waves=0, resume=-1, kinds=0, suspend_lanes=0, leaf_lanes=0, chunk_spp=0)
+
+
 # every symbol include/rt_api.h declares (checked by tests/test_abi.py)
 EXPORTS = {
     "rt_scene_create": (C.c_int, [C.POINTER(rt_scene_desc), C.POINTER(C.c_void_p)]),
     "rt_scene_destroy": (None, [C.c_void_p]),
     "rt_scene_get_info": (C.c_int, [C.c_void_p, C.POINTER(rt_scene_info)]),
+    "rt_scene_set_tuning": (C.c_int, [C.c_void_p, C.POINTER(rt_tuning)]),
+    "rt_scene_get_tuning": (C.c_int, [C.c_void_p, C.POINTER(rt_tuning)]),
+    "rt_scene_sample_chunks": (C.c_int, [C.c_void_p, C.POINTER(rt_render_params), C.POINTER(C.c_uint32),
+                                         C.POINTER(C.c_uint32)]),
     "rt_render": (C.c_int, [C.c_void_p, C.POINTER(rt_render_params), C.c_void_p, C.c_void_p, C.POINTER(rt_stats)]),
     "rt_tiles_per_rank": (C.c_int, [C.POINTER(rt_render_params), C.c_uint32, C.POINTER(C.c_uint32)]),
     "rt_sample_chunks": (C.c_int, [C.POINTER(rt_render_params), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
@@ -129,6 +141,7 @@ EXPORTS = {
     "rt_parsed_scene_free": (None, [C.c_void_p]),
     "rt_tonemap_gamma": (None, [C.c_void_p, C.c_uint64, C.c_void_p]),
     "rt_save_ppm": (C.c_int, [C.c_char_p, C.c_uint32, C.c_uint32, C.c_void_p]),
+    "rt_byte_thresholds": (C.c_int, [C.c_void_p]),
     "rt_last_error": (C.c_char_p, []),
     "rt_api_version": (C.c_int, []),
     "rt_device_count": (C.c_int, []),
@@ -363,6 +376,28 @@ class Scene:
         out["bvh_depth"] = list(i.bvh_depth)
         return out
 
+    def set_tuning(self, **kw):
+        """Force the kernel form of this scene's renders (rt_scene_set_tuning): waves (3|4),
+        resume (0|1), kinds (3 = all-kinds instance), suspend_lanes, leaf_lanes (1..64),
+        chunk_spp.  Fields not given are auto (the library's per-scene pick)."""
+        bad = set(kw) - set(TUNING_AUTO)
+        if bad:
+            raise ValueError(f"unknown tuning fields {sorted(bad)}")
+        t = rt_tuning(**{**TUNING_AUTO, **{k: int(v) for k, v in kw.items()}})
+        _check(lib().rt_scene_set_tuning(self._h, C.byref(t)))
+
+    def tuning(self) -> dict:
+        """The resolved kernel form the next render runs (rt_scene_get_tuning)."""
+        t = rt_tuning()
+        _check(lib().rt_scene_get_tuning(self._h, C.byref(t)))
+        return {k: getattr(t, k) for k, _ in t._fields_}
+
+    def sample_chunks(self, params: RenderParams):
+        """(chunks, chunk_spp) this scene's renders use (rt_scene_sample_chunks)."""
+        k, cs = C.c_uint32(), C.c_uint32()
+        _check(lib().rt_scene_sample_chunks(self._h, C.byref(params.to_c()), C.byref(k), C.byref(cs)))
+        return k.value, cs.value
+
     def generate_image(self, params: RenderParams, hit_ids: bool = False, stats: bool = False):
         """Mean radiance per pixel [H, W, 3] f64 (main.rs:100-104 before tonemapping).
 
@@ -545,6 +580,13 @@ def build_bvh(boxes: np.ndarray):
                               links.ctypes.data_as(C.c_void_p), bounds.ctypes.data_as(C.c_void_p),
                               order.ctypes.data_as(C.c_void_p), C.byref(depth)))
     return links, bounds, order, depth.value
+
+
+def byte_thresholds() -> np.ndarray:
+    """The device epilogue's 255 byte thresholds on the tonemapped value (host only)."""
+    out = np.zeros(255, np.float64)
+    _check(lib().rt_byte_thresholds(out.ctypes.data_as(C.c_void_p)))
+    return out
 
 
 def sample_chunks(params: RenderParams):

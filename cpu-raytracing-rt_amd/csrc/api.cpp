@@ -65,6 +65,8 @@ struct rt_scene {
     // stream wait on it, then re-records it, so calls issued on different
     // streams never overlap on the shared workspace.
     hipEvent_t ws_done = nullptr;
+    // requested kernel form (rt_scene_set_tuning); auto fields resolve per scene
+    rt_tuning tune{0, -1, 0, 0, 0, 0};
 };
 
 namespace {
@@ -166,22 +168,19 @@ int check_params(const rt_render_params* p) {
     return RT_OK;
 }
 
-// Sample chunking of a frame (render.h sample_chunks).  RT_CHUNK_SPP=<n>
-// overrides the run length for tuning experiments only; rt_sample_chunks
-// reports the override too, so checkers stay consistent.
-void frame_chunks(const rt_render_params* p, uint32_t& chunks, uint32_t& chunk_spp) {
+// Sample chunking of a frame (render.h sample_chunks); a scene's tuning may
+// force the run length (rt_tuning.chunk_spp, tests and tuning experiments;
+// rt_scene_sample_chunks reports it, so checkers stay consistent).
+void frame_chunks(const rt_render_params* p, uint32_t force_spp, uint32_t& chunks, uint32_t& chunk_spp) {
     sample_chunks(p->width, p->height, p->spp, chunks, chunk_spp);
-    if (const char* e = std::getenv("RT_CHUNK_SPP")) {
-        const long v = std::strtol(e, nullptr, 10);
-        if (v > 0) {
-            chunk_spp = (uint32_t)std::min<long>(v, p->spp);
-            chunks = (p->spp + chunk_spp - 1) / chunk_spp;
-        }
+    if (force_spp > 0) {
+        chunk_spp = std::min(force_spp, p->spp);
+        chunks = (p->spp + chunk_spp - 1) / chunk_spp;
     }
 }
 
 // Camera::new (camera.rs:17-46) on the host + the tile map of one rank.
-KParams make_kparams(const rt_render_params* p, uint32_t rank, uint32_t world) {
+KParams make_kparams(const rt_render_params* p, uint32_t rank, uint32_t world, uint32_t force_spp = 0) {
     KParams k;
     std::memset(&k, 0, sizeof(k));
     k.width = p->width; k.height = p->height; k.spp = p->spp; k.ray_depth = p->ray_depth;
@@ -208,7 +207,7 @@ KParams make_kparams(const rt_render_params* p, uint32_t rank, uint32_t world) {
     k.tiles_y = (p->height + RT_TILE - 1) / RT_TILE;
     k.n_tiles = (uint64_t)k.tiles_x * k.tiles_y;
     k.n_slots = (uint32_t)((k.n_tiles + world - 1) / world);
-    frame_chunks(p, k.chunks, k.chunk_spp);
+    frame_chunks(p, force_spp, k.chunks, k.chunk_spp);
     return k;
 }
 
@@ -252,12 +251,9 @@ int ensure_spill(rt_scene* s, uint64_t lanes) {
 // Register budget of the path kernel for this scene.  Large BVHs make the loop
 // latency-bound on dependent node loads, where a 4th wave per SIMD hides more
 // than its register spill costs (C3: -9%); small scenes are VALU-bound and run
-// best at 3 (C2: +2% at 4).  RT_WAVES=3|4 forces one (tests, tuning).
+// best at 3 (C2: +2% at 4).  rt_tuning.waves forces one (tests, tuning).
 uint32_t path_waves(const rt_scene* s) {
-    if (const char* e = std::getenv("RT_WAVES")) {
-        const long v = std::strtol(e, nullptr, 10);
-        if (v == 3 || v == 4) return (uint32_t)v;
-    }
+    if (s->tune.waves) return s->tune.waves;
     uint64_t nodes = 0;
     for (int k = 0; k < 6; ++k) nodes += s->info.bvh_nodes[k];
     return nodes > kDeepSceneNodes ? 4u : 3u;
@@ -267,11 +263,9 @@ uint32_t path_waves(const rt_scene* s) {
 // deep triangle BVH, where a wave's traversal loop otherwise runs most trips
 // with few live lanes (C3: 43%); scenes without one keep the fused segment,
 // which carries less state across the loop (C2: 113 vs 130 ms at 64 spp).
-// RT_RESUME=0|1 forces one (tests, tuning).
+// rt_tuning.resume forces one (tests, tuning).
 bool path_resume(const rt_scene* s) {
-    if (const char* e = std::getenv("RT_RESUME")) {
-        if (e[0] == '0' || e[0] == '1') return e[0] == '1';
-    }
+    if (s->tune.resume >= 0) return s->tune.resume == 1;
     return s->info.bvh_nodes[2] > kDeepSceneNodes;
 }
 
@@ -280,11 +274,9 @@ bool path_resume(const rt_scene* s) {
 // code or state for the other kind: triangle-only ones (every glTF scene) the
 // 4-wave resumable kernel without a shape candidate carried across its loop
 // (C3 -6%), shape-only ones (the Cornell box) the fused kernel without triangle
-// traversal.  RT_KINDS=3 forces the general instances (tests, tuning).
+// traversal.  rt_tuning.kinds = 3 forces the general instances (tests, tuning).
 int path_kinds(const rt_scene* s) {
-    if (const char* e = std::getenv("RT_KINDS")) {
-        if (e[0] == '3') return 3;
-    }
+    if (s->tune.kinds == 3) return 3;
     const DevScene& d = s->dev;
     const bool shapes = d.n_planes || d.boxes.n_prims || d.ells.n_prims || d.lboxes.n_prims || d.lells.n_prims;
     const bool tris = d.tris.n_prims || d.ltris.n_prims;
@@ -293,27 +285,21 @@ int path_kinds(const rt_scene* s) {
 
 // Suspend threshold of the resumable traversal (render.h kSuspendCached /
 // kSuspendStreamed): by whether the triangle BVH and its hot records fit the
-// Infinity Cache.  RT_SUSPEND_LANES=<n> forces one (tuning).
+// Infinity Cache.  rt_tuning.suspend_lanes forces one (tuning).
 bool bvh_streamed(const rt_scene* s) {  // the triangle BVH and its hot records exceed the Infinity Cache
     const uint64_t bytes = s->info.bvh_nodes[2] * sizeof(DevNode) + s->info.n_triangles * sizeof(DevTri);
     return bytes > kCacheBytes;
 }
 uint32_t path_suspend(const rt_scene* s) {
-    if (const char* e = std::getenv("RT_SUSPEND_LANES")) {
-        const long v = std::strtol(e, nullptr, 10);
-        if (v >= 1 && v <= 64) return (uint32_t)v;
-    }
+    if (s->tune.suspend_lanes) return s->tune.suspend_lanes;
     return bvh_streamed(s) ? kSuspendStreamed : kSuspendCached;
 }
 
 // Leaf batch of the resumable traversal (render.hip trav_step: lanes waiting at
 // leaves before the wave tests them), by the same cache criterion as the suspend
-// threshold (render.h kLeafCached / kLeafStreamed).  RT_LEAF_LANES=<n> forces one.
+// threshold (render.h kLeafCached / kLeafStreamed).  rt_tuning.leaf_lanes forces one.
 uint32_t path_leaf_batch(const rt_scene* s) {
-    if (const char* e = std::getenv("RT_LEAF_LANES")) {
-        const long v = std::strtol(e, nullptr, 10);
-        if (v >= 1 && v <= 64) return (uint32_t)v;
-    }
+    if (s->tune.leaf_lanes) return s->tune.leaf_lanes;
     return bvh_streamed(s) ? kLeafStreamed : kLeafCached;
 }
 
@@ -508,7 +494,37 @@ int rt_sample_chunks(const rt_render_params* p, uint32_t* chunks, uint32_t* chun
     int rc = check_params(p);
     if (rc) return rc;
     if (!chunks || !chunk_spp) return set_error(RT_ERR_INVALID, "output is NULL");
-    frame_chunks(p, *chunks, *chunk_spp);
+    frame_chunks(p, 0, *chunks, *chunk_spp);
+    return RT_OK;
+}
+
+int rt_scene_sample_chunks(const rt_scene* s, const rt_render_params* p, uint32_t* chunks, uint32_t* chunk_spp) {
+    int rc = check_params(p);
+    if (rc) return rc;
+    if (!s || !chunks || !chunk_spp) return set_error(RT_ERR_INVALID, "scene/output is NULL");
+    frame_chunks(p, s->tune.chunk_spp, *chunks, *chunk_spp);
+    return RT_OK;
+}
+
+int rt_scene_set_tuning(rt_scene* s, const rt_tuning* t) {
+    if (!s) return set_error(RT_ERR_INVALID, "scene is NULL");
+    if (!t) { s->tune = rt_tuning{0, -1, 0, 0, 0, 0}; return RT_OK; }
+    if (t->waves != 0 && t->waves != 3 && t->waves != 4) return set_error(RT_ERR_INVALID, "waves must be 0, 3 or 4");
+    if (t->resume < -1 || t->resume > 1) return set_error(RT_ERR_INVALID, "resume must be -1, 0 or 1");
+    if (t->kinds != 0 && t->kinds != 3) return set_error(RT_ERR_INVALID, "kinds must be 0 or 3");
+    if (t->suspend_lanes > 64 || t->leaf_lanes > 64) return set_error(RT_ERR_INVALID, "lane counts must be <= 64");
+    s->tune = *t;
+    return RT_OK;
+}
+
+int rt_scene_get_tuning(const rt_scene* s, rt_tuning* out) {
+    if (!s || !out) return set_error(RT_ERR_INVALID, "scene/out is NULL");
+    out->waves = path_waves(s);
+    out->resume = path_resume(s) ? 1 : 0;
+    out->kinds = (uint32_t)path_kinds(s);
+    out->suspend_lanes = path_suspend(s);
+    out->leaf_lanes = path_leaf_batch(s);
+    out->chunk_spp = s->tune.chunk_spp;
     return RT_OK;
 }
 
@@ -519,7 +535,7 @@ int rt_render_tiles_async(rt_scene* s, const rt_render_params* p, uint32_t rank,
     if (!s || !d_tile_rgb) return set_error(RT_ERR_INVALID, "scene/output is NULL");
     if (world == 0 || rank >= world) return set_error(RT_ERR_INVALID, "rank must be < world");
     DEVICE_GUARD(s);
-    KParams k = make_kparams(p, rank, world);
+    KParams k = make_kparams(p, rank, world, s->tune.chunk_spp);
     const bool want_stats = (p->flags & RT_FLAG_STATS) != 0;
     PathWork W;
     if ((rc = prepare_path(s, k, want_stats, false, W))) return rc;
@@ -584,7 +600,7 @@ int rt_render(rt_scene* s, const rt_render_params* p, double* out_mean_rgb, int3
     if (rc) return rc;
     if (!s || !out_mean_rgb) return set_error(RT_ERR_INVALID, "scene/output is NULL");
     DEVICE_GUARD(s);
-    KParams k = make_kparams(p, 0, 1);
+    KParams k = make_kparams(p, 0, 1, s->tune.chunk_spp);
     const uint32_t slots = slots_per_rank(k);
     const uint64_t npx = (uint64_t)p->width * p->height;
     const bool want_hits = opt_hit_ids && (p->flags & RT_FLAG_HIT_IDS);

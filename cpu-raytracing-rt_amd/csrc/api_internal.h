@@ -9,6 +9,11 @@ namespace rt {
 
 int set_error(int code, const std::string& msg);  // records rt_last_error, returns code
 
+// post.cpp: the 255 byte thresholds of the gamma + PPM quantisation on a
+// tonemapped value, derived from the host pow and proven exact; false if the
+// proof fails (the device epilogue then uses its own pow).
+bool byte_thresholds(double thr[255]);
+
 struct HostScene;
 // rt_scene_create in two halves (api.cpp): the host build (six BVHs, flattened
 // records) and the upload of that build to the current HIP device, so a

@@ -48,6 +48,7 @@ struct Rccl {
     void* handle = nullptr;
     decltype(&ncclCommInitAll) comm_init_all = nullptr;
     decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclCommAbort) comm_abort = nullptr;
     decltype(&ncclGather) gather = nullptr;
     decltype(&ncclGroupStart) group_start = nullptr;
     decltype(&ncclGroupEnd) group_end = nullptr;
@@ -56,11 +57,13 @@ struct Rccl {
     bool bind(void* h) {
         comm_init_all = (decltype(comm_init_all))dlsym(h, "ncclCommInitAll");
         comm_destroy = (decltype(comm_destroy))dlsym(h, "ncclCommDestroy");
+        comm_abort = (decltype(comm_abort))dlsym(h, "ncclCommAbort");
         gather = (decltype(gather))dlsym(h, "ncclGather");
         group_start = (decltype(group_start))dlsym(h, "ncclGroupStart");
         group_end = (decltype(group_end))dlsym(h, "ncclGroupEnd");
         error_string = (decltype(error_string))dlsym(h, "ncclGetErrorString");
-        if (!comm_init_all || !comm_destroy || !gather || !group_start || !group_end || !error_string) return false;
+        if (!comm_init_all || !comm_destroy || !comm_abort || !gather || !group_start || !group_end || !error_string)
+            return false;
         handle = h;
         return true;
     }
@@ -115,6 +118,7 @@ struct rt_multi {
     bool peer = false;
     Rccl rccl;
     std::vector<ncclComm_t> comms;
+    bool comms_aborted = false;               // a failed gather aborted them: the handle cannot gather again
 };
 
 namespace {
@@ -145,6 +149,21 @@ void free_multi(rt_multi* m) {
 
 struct MultiDeleter {
     void operator()(rt_multi* m) const { free_multi(m); }
+};
+
+// Error return after work was queued: wait for every device's stream (so no
+// launch of this frame is left running against buffers the caller may free),
+// errors ignored — the call already failed.  Disarmed on success.
+struct Drain {
+    rt_multi* m;
+    bool armed = false;
+    ~Drain() {
+        if (!armed) return;
+        for (size_t i = 0; i < m->devs.size(); ++i) {
+            (void)hipSetDevice(m->devs[i]);
+            (void)hipStreamSynchronize(m->streams[i]);
+        }
+    }
 };
 
 }  // namespace
@@ -210,6 +229,9 @@ int rt_multi_render(rt_multi* m, const rt_render_params* p, double* out_mean_rgb
     if (!m || !p) return set_error(RT_ERR_INVALID, "multi/params is NULL");
     if (!out_mean_rgb && !out_ppm_bytes) return set_error(RT_ERR_INVALID, "no output requested");
     if (p->flags & RT_FLAG_HIT_IDS) return set_error(RT_ERR_INVALID, "hit-id dumps are rt_render's (one device)");
+    if (m->comms_aborted)
+        return set_error(RT_ERR_DEVICE, "a previous gather failed and aborted the RCCL communicators: "
+                                        "destroy and recreate the rt_multi handle");
     const uint32_t n = (uint32_t)m->devs.size();
     uint32_t slots = 0;
     if (int rc = rt_tiles_per_rank(p, n, &slots)) return rc;  // also validates params
@@ -236,7 +258,10 @@ int rt_multi_render(rt_multi* m, const rt_render_params* p, double* out_mean_rgb
     if (out_ppm_bytes)
         if (int rc = grow(m->bytes, m->bytes_cap, 3 * npx)) return rc;
 
-    // every share on its own device and stream (the launches overlap across devices)
+    // every share on its own device and stream (the launches overlap across devices);
+    // from here on an error return first drains every stream
+    Drain drain{m};
+    drain.armed = true;
     for (uint32_t i = 0; i < n; ++i) {
         MHIP(hipSetDevice(m->devs[i]));
         MHIP(hipEventRecord(m->ev0[i], m->streams[i]));
@@ -257,8 +282,14 @@ int rt_multi_render(rt_multi* m, const rt_render_params* p, double* out_mean_rgb
             r = m->rccl.gather(m->tiles[i], i == 0 ? m->gathered : nullptr, cnt, ncclFloat64, 0, m->comms[i],
                                m->streams[i]);
         const ncclResult_t r2 = m->rccl.group_end();
-        if (r != ncclSuccess || r2 != ncclSuccess)
+        if (r != ncclSuccess || r2 != ncclSuccess) {
+            // ranks already enqueued would wait forever on a collective the others never
+            // join: abort the communicators (not destroy) before the streams are drained
+            for (ncclComm_t& c : m->comms)
+                if (c) { (void)m->rccl.comm_abort(c); c = nullptr; }
+            m->comms_aborted = true;
             return set_error(RT_ERR_DEVICE, std::string("ncclGather: ") + m->rccl.error_string(r ? r : r2));
+        }
     }
     // root: unpack (main.rs:96-104) and/or the fused tonemap + PPM bytes, then one D2H copy each
     MHIP(hipSetDevice(m->devs[0]));
@@ -293,6 +324,7 @@ int rt_multi_render(rt_multi* m, const rt_render_params* p, double* out_mean_rgb
         opt_stats->kernel_ms = kern_ms;
         opt_stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
+    drain.armed = false;
     return RT_OK;
 }
 

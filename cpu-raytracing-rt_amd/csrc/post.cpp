@@ -2,7 +2,9 @@
 // and the binary P6 PPM writer (ppm.rs:4-19), applied to the mean radiance
 // that rt_render returns, exactly where main.rs:104 / :74 apply them.
 #include <cmath>
+#include <cstdint>
 #include <cstdio>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -26,7 +28,65 @@ unsigned char to_byte(double v) {  // float_to_byte (ppm.rs:13-15)
     return (unsigned char)r;
 }
 
+// The PPM byte of a tonemapped value a (main.rs:104 correct_gamma, then ppm.rs:13-15)
+unsigned char gamma_byte(double a) { return to_byte(std::pow(a, 1.0 / 2.2)); }
+
+double from_bits(uint64_t b) {
+    double d;
+    std::memcpy(&d, &b, 8);
+    return d;
+}
+uint64_t to_bits(double d) {
+    uint64_t b;
+    std::memcpy(&b, &d, 8);
+    return b;
+}
+
 }  // namespace
+
+namespace rt {
+
+// thr[k - 1] = the least double a >= 0 with gamma_byte(a) >= k, k = 1..255, so
+// for every tonemapped value a (aces() is in [0, 1], -0 or NaN) the byte is the
+// number of thresholds <= a — what the device epilogue computes by a binary
+// search (post_dev.hip), with the host's own `pow` behind every threshold.
+//
+// Found by bisection over the bit patterns of [0, 1] (non-negative doubles
+// order like their bits), then proven: the byte is a monotone function of v =
+// pow(a, 1/2.2) (a product by 255 and round, both monotone), and glibc's pow is
+// within 1 ulp of the monotone exact power, so the predicate "byte >= k" can
+// disagree with "a >= thr" only where the exact power is within ~1 ulp of the
+// byte boundary — a run of a few ulps of a around the bisection point.  Every
+// double within kWin ulps on either side is checked, so the table is exact for
+// all inputs or the function reports failure (the device then keeps its own
+// pow: post_dev.hip).
+bool byte_thresholds(double thr[255]) {
+    constexpr uint64_t kWin = 512;
+    const uint64_t one = to_bits(1.0);
+    for (int k = 1; k <= 255; ++k) {
+        uint64_t lo = 0, hi = one;  // gamma_byte(0) = 0 < k <= 255 = gamma_byte(1)
+        while (hi - lo > 1) {
+            const uint64_t mid = lo + (hi - lo) / 2;
+            if (gamma_byte(from_bits(mid)) >= k) hi = mid;
+            else lo = mid;
+        }
+        for (uint64_t i = 1; i <= kWin; ++i) {
+            if (i <= hi && gamma_byte(from_bits(hi - i)) >= k) return false;
+            if (hi + i - 1 <= one && gamma_byte(from_bits(hi + i - 1)) < k) return false;
+        }
+        thr[k - 1] = from_bits(hi);
+        if (k > 1 && !(thr[k - 2] < thr[k - 1])) return false;
+    }
+    return true;
+}
+
+}  // namespace rt
+
+extern "C" int rt_byte_thresholds(double* out) {
+    if (!out) return rt::set_error(RT_ERR_INVALID, "out is NULL");
+    if (!rt::byte_thresholds(out)) return rt::set_error(RT_ERR_UNSUPPORTED, "host pow: byte thresholds not provable");
+    return RT_OK;
+}
 
 extern "C" void rt_tonemap_gamma(const double* in, uint64_t n, double* out) {
     if (!in || !out) return;

@@ -42,14 +42,21 @@ constexpr int kPhaseWord0 = 16;   // RT_PHASES builds: region cycles + loop coun
 // work units or the chunks would still hold >= kMinChunkSpp samples (many short
 // wave-tiles balance the ranks of a multi-GPU frame; the path kernel streams
 // rows across wave-tiles, so short ones cost no drain), capped at spp and
-// kMaxChunks, then trimmed so no chunk is empty.
+// kMaxChunks, and by kPartBytes: the chunk partial sums ([tiles][chunks][256][3]
+// f64, written and reduced once per frame) stay within 4 GiB over all ranks
+// (C2/C3: 32 chunks, 1.6 GB; C4 3840x2160: 16 chunks, 3.2 GB — 64 would be
+// 12.7 GB); then trimmed so no chunk is empty.
 constexpr uint64_t kChunkLanes = 32000000;
 constexpr uint32_t kMinChunkSpp = 8;
 constexpr uint32_t kMaxChunks = 64;
+constexpr uint64_t kPartBytes = 4ull << 30;
 inline void sample_chunks(uint32_t W, uint32_t H, uint32_t spp, uint32_t& chunks, uint32_t& chunk_spp) {
     const uint64_t px = (uint64_t)W * H;
+    const uint64_t chunk_bytes = (uint64_t)((W + 15) / 16) * ((H + 15) / 16) * 256 * 3 * sizeof(double);
     uint32_t k = 1;
-    while (k * 2 <= spp && k < kMaxChunks && (px * k < kChunkLanes || spp / (k * 2) >= kMinChunkSpp)) k *= 2;
+    while (k * 2 <= spp && k < kMaxChunks && chunk_bytes * (k * 2) <= kPartBytes &&
+           (px * k < kChunkLanes || spp / (k * 2) >= kMinChunkSpp))
+        k *= 2;
     chunk_spp = (spp + k - 1) / k;
     chunks = (spp + chunk_spp - 1) / chunk_spp;
 }

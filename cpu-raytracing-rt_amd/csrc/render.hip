@@ -1040,7 +1040,9 @@ RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, P
     // ids are the same bits); the stats build (ST) still runs it, so the work
     // counters stay the oracle's (whose light query on the last bounce the SURVEY
     // byte model counts).
+#ifndef RT_NO_LASTSEG  // ablation build: the last segment shades like every other
     if (!ST && last) return false;
+#endif
     rng_align(rng);   // shading draws start on a block boundary (oracle.c rng_align)
     rng_top_up(rng);  // every hit lane here: a coherent refill point
     const V3 o = ps.o, d = ps.d;

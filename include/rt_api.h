@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RT_API_VERSION 3
+#define RT_API_VERSION 4
 
 typedef enum rt_error {
     RT_OK = 0,
@@ -186,6 +186,26 @@ typedef struct rt_scene_info {
 } rt_scene_info;
 int rt_scene_get_info(const rt_scene* scene, rt_scene_info* out);
 
+/* Kernel form of a scene's renders.  The library picks every
+   field from the scene itself ("auto"); a caller may force one for tests and
+   tuning.  The library reads no environment variables: the resolved form is a
+   property of the scene handle, reported by rt_scene_get_tuning, so every rank
+   and process rendering one frame runs the same kernel instance. */
+typedef struct rt_tuning {
+    uint32_t waves;          /* 0 auto (4 when the BVHs hold > 4096 nodes, else 3); 3 or 4 waves/SIMD  */
+    int32_t  resume;         /* -1 auto (1 for a triangle BVH of > 4096 nodes); 0 fused segment,
+                                1 resumable triangle traversal                                          */
+    uint32_t kinds;          /* 0 auto (the scene's primitive kinds); 3 the all-kinds instance          */
+    uint32_t suspend_lanes;  /* 0 auto (24 cache-resident BVH, 40 HBM-streamed); 1..64                   */
+    uint32_t leaf_lanes;     /* 0 auto (32 cache-resident BVH, 24 HBM-streamed); 1..64                   */
+    uint32_t chunk_spp;      /* 0 the frame's rule (rt_sample_chunks); else the sample run length        */
+} rt_tuning;
+/* NULL restores every field to auto.  Fields out of range -> RT_ERR_INVALID. */
+int rt_scene_set_tuning(rt_scene* scene, const rt_tuning* tuning);
+/* The form the next render of this scene runs: auto fields resolved (chunk_spp
+   stays 0 when the frame's rule applies). */
+int rt_scene_get_tuning(const rt_scene* scene, rt_tuning* resolved);
+
 /* ======================= the frame (hot path) ============================= */
 /* Replaces generate_image's pixel loop (src/main.rs:85-103): for every pixel,
    the mean over spp of raytrace(Camera::fuzzy_ray(px)) (camera.rs:48-55,
@@ -222,6 +242,10 @@ int rt_read_raw_stats(rt_scene* scene, uint64_t* out, uint32_t n);
    sequential sum; otherwise the result differs from it by f64 reassociation only
    (no replacement for main.rs; exposed so checkers can reproduce the order). */
 int rt_sample_chunks(const rt_render_params* params, uint32_t* chunks, uint32_t* chunk_spp);
+/* The chunking this scene's renders use: rt_sample_chunks unless its tuning
+   forces a run length (rt_tuning.chunk_spp). */
+int rt_scene_sample_chunks(const rt_scene* scene, const rt_render_params* params, uint32_t* chunks,
+                           uint32_t* chunk_spp);
 /* Work counters accumulated on the device by every rt_render_tiles_async call
    made with RT_FLAG_STATS since the last reset (synchronises the device). */
 int rt_read_stats(rt_scene* scene, rt_stats* out, int reset);
@@ -231,9 +255,11 @@ int rt_unpack_tiles_async(const rt_render_params* params, uint32_t world,
                           const double* d_gathered, double* d_image, void* hip_stream);
 /* The same unpack fused with correct_gamma(aces_tonemap(.)) and the PPM byte
    quantisation (main.rs:104, postprocessing.rs:5-37, ppm.rs:13-19): d_bytes is
-   the P6 payload [H][W][3] u8, so the f64 image never leaves the device.  Uses
-   the device `pow`, which may round differently from the host libm in the last
-   ulp (a byte can move only on a .5 boundary; see tests/test_gpu_post.py). */
+   the P6 payload [H][W][3] u8, so the f64 image never leaves the device.  The
+   bytes are the host path's (rt_tonemap_gamma + rt_save_ppm) bit for bit: the
+   device computes aces_tonemap with the same IEEE operations, and the gamma +
+   quantisation step is a search over 255 thresholds on the tonemapped value
+   that the host derives from its own `pow` (post.cpp byte_thresholds). */
 int rt_unpack_tiles_bytes_async(const rt_render_params* params, uint32_t world,
                                 const double* d_gathered, uint8_t* d_bytes, void* hip_stream);
 /* Device tonemap + gamma + PPM bytes of a mean-radiance image already in HBM
@@ -325,6 +351,11 @@ void rt_parsed_scene_free(rt_parsed_scene* ps);
 void rt_tonemap_gamma(const double* mean_rgb, uint64_t n_pixels, double* out_rgb);
 /* Binary P6 PPM of an already tonemapped image (ppm.rs:4-19). */
 int rt_save_ppm(const char* path, uint32_t width, uint32_t height, const double* rgb);
+/* The device epilogue's table (host only): out[k-1] = the least tonemapped
+   value a >= 0 whose PPM byte round(clamp(pow(a, 1/2.2))*255) is >= k, k =
+   1..255, derived from this library's host pow and proven exact
+   (RT_ERR_UNSUPPORTED if the proof fails). */
+int rt_byte_thresholds(double* out255);
 
 /* ======================= misc ============================================= */
 const char* rt_last_error(void);

@@ -301,7 +301,7 @@ static AABB rotated_aabb(AABB a, Q r) { /* scene.rs:255-268 */
 }
 
 /* ---- BVH build (bvh.rs:11-17, 75-140, 224-256) ------------------------- */
-typedef struct { const AABB* boxes; int axis; } SortCtx;
+typedef struct { const int64_t* key; } SortCtx;  /* total_order_key of each primitive's midpoint on one axis */
 static inline double axis_of(V3 v, int axis) { return vget(v, axis); }
 static inline int64_t total_order_key(double x) { /* f64::total_cmp */
     int64_t b; memcpy(&b, &x, 8);
@@ -313,12 +313,28 @@ static inline int64_t total_order_key(double x) { /* f64::total_cmp */
 static int cmp_mid(const void* pa, const void* pb, void* pctx) {
     const SortCtx* c = (const SortCtx*)pctx;
     uint64_t ia = *(const uint64_t*)pa, ib = *(const uint64_t*)pb;
-    double ma = (axis_of(c->boxes[ia].min, c->axis) + axis_of(c->boxes[ia].max, c->axis)) / 2.0;
-    double mb = (axis_of(c->boxes[ib].min, c->axis) + axis_of(c->boxes[ib].max, c->axis)) / 2.0;
-    int64_t ka = total_order_key(ma), kb = total_order_key(mb);
+    int64_t ka = c->key[ia], kb = c->key[ib];
     if (ka < kb) return -1;
     if (ka > kb) return 1;
     return ia < ib ? -1 : (ia > ib ? 1 : 0);
+}
+/* Sort by cmp_mid: a parallel merge sort (OpenMP tasks) above 1M elements.
+   cmp_mid is a total order (midpoint key, then list index), so every correct
+   sort gives the same permutation as qsort_r. */
+static void psort(uint64_t* a, uint64_t n, const int64_t* key, uint64_t* tmp) {
+    SortCtx ctx = {key};
+    if (n < (1u << 20)) { qsort_r(a, n, sizeof(uint64_t), cmp_mid, &ctx); return; }
+    const uint64_t h = n / 2;
+#pragma omp task
+    psort(a, h, key, tmp);
+#pragma omp task
+    psort(a + h, n - h, key, tmp + h);
+#pragma omp taskwait
+    uint64_t i = 0, j = h, k = 0;
+    while (i < h && j < n) tmp[k++] = cmp_mid(&a[j], &a[i], &ctx) < 0 ? a[j++] : a[i++];
+    while (i < h) tmp[k++] = a[i++];
+    while (j < n) tmp[k++] = a[j++];
+    memcpy(a, tmp, n * sizeof(uint64_t));
 }
 static inline double aabb_score(const AABB* a) { /* bvh.rs:115-118 */
     V3 s = vsub(a->max, a->min);
@@ -327,7 +343,18 @@ static inline double aabb_score(const AABB* a) { /* bvh.rs:115-118 */
 typedef struct {
     const AABB* boxes; uint64_t* idx; Node* nodes; uint64_t n_nodes, cap;
     AABB* fwd; AABB* bwd; uint32_t max_depth;
+    const int64_t* keys[3];  /* midpoint sort keys per axis (computed once per build) */
 } Builder;
+static void sort_mid(Builder* b, uint64_t lo, uint64_t n, int axis) {
+    if (n < (1u << 20)) {
+        SortCtx ctx = {b->keys[axis]};
+        qsort_r(b->idx + lo, n, sizeof(uint64_t), cmp_mid, &ctx);
+        return;
+    }
+    uint64_t* tmp = (uint64_t*)malloc(n * sizeof(uint64_t));
+    psort(b->idx + lo, n, b->keys[axis], tmp);
+    free(tmp);
+}
 static uint64_t push_node(Builder* b, Node n) {
     if (b->n_nodes == b->cap) {
         b->cap = b->cap ? b->cap * 2 : 64;
@@ -336,6 +363,11 @@ static uint64_t push_node(Builder* b, Node n) {
     b->nodes[b->n_nodes] = n;
     return b->n_nodes++;
 }
+/* Subtrees of at least this many primitives build their two children as
+   parallel OpenMP tasks (the 10M-triangle C5 tree: minutes -> about a minute). */
+enum { kParMin = 65536 };
+static void build_sub(const Builder* parent, uint64_t lo, uint64_t hi, uint32_t depth, Builder* out);
+static uint64_t splice(Builder* b, Builder* sub);
 static uint64_t build_nodes(Builder* b, uint64_t lo, uint64_t hi, uint32_t depth) { /* bvh.rs:75-113 */
     uint64_t n = hi - lo;
     if (depth > b->max_depth) b->max_depth = depth;
@@ -349,8 +381,7 @@ static uint64_t build_nodes(Builder* b, uint64_t lo, uint64_t hi, uint32_t depth
     double best_score = aabb_score(&box) * (double)n;
     int best_axis = -1;
     for (int axis = 0; axis < 3; ++axis) { /* subdivision_score (bvh.rs:120-135) */
-        SortCtx ctx = {b->boxes, axis};
-        qsort_r(b->idx + lo, n, sizeof(uint64_t), cmp_mid, &ctx);
+        sort_mid(b, lo, n, axis);
         /* AABBSplitsBuilder::make_splits (bvh.rs:238-255) */
         AABB acc = aabb_empty();
         for (uint64_t i = 0; i + 1 < n; ++i) { aabb_extend_aabb(&acc, &b->boxes[b->idx[lo + i]]); b->fwd[i] = acc; }
@@ -366,25 +397,71 @@ static uint64_t build_nodes(Builder* b, uint64_t lo, uint64_t hi, uint32_t depth
         Node leaf = {box, -1, -1, lo, hi};
         return push_node(b, leaf);
     }
-    SortCtx ctx = {b->boxes, best_axis};
-    qsort_r(b->idx + lo, n, sizeof(uint64_t), cmp_mid, &ctx);
+    sort_mid(b, lo, n, best_axis);
     Node placeholder = {box, -1, -1, 0, 0};
     uint64_t me = push_node(b, placeholder);
-    uint64_t l = build_nodes(b, lo, lo + best_first, depth + 1);
-    uint64_t r = build_nodes(b, lo + best_first, hi, depth + 1);
+    uint64_t l, r;
+    if (n >= kParMin) { /* both subtrees at once (OpenMP tasks), spliced in pre-order */
+        Builder L, R;
+#pragma omp task shared(L)
+        build_sub(b, lo, lo + best_first, depth + 1, &L);
+#pragma omp task shared(R)
+        build_sub(b, lo + best_first, hi, depth + 1, &R);
+#pragma omp taskwait
+        l = splice(b, &L);
+        r = splice(b, &R);
+    } else {
+        l = build_nodes(b, lo, lo + best_first, depth + 1);
+        r = build_nodes(b, lo + best_first, hi, depth + 1);
+    }
     b->nodes[me].left = (int64_t)l;
     b->nodes[me].right = (int64_t)r;
     return me;
+}
+/* A subtree built on its own (node indices from 0, own sort scratch).  The
+   tree is the sequential build's: every node's split depends only on its own
+   primitive range, and pre-order is parent, left subtree, right subtree. */
+static void build_sub(const Builder* parent, uint64_t lo, uint64_t hi, uint32_t depth, Builder* out) {
+    const uint64_t n = hi - lo;
+    Builder b = {parent->boxes, parent->idx, NULL, 0, 0, NULL, NULL, 0, {parent->keys[0], parent->keys[1], parent->keys[2]}};
+    b.fwd = (AABB*)malloc(sizeof(AABB) * (n > 1 ? n - 1 : 1));
+    b.bwd = (AABB*)malloc(sizeof(AABB) * (n > 1 ? n - 1 : 1));
+    build_nodes(&b, lo, hi, depth);
+    free(b.fwd); free(b.bwd);
+    b.fwd = b.bwd = NULL;
+    *out = b;
+}
+static uint64_t splice(Builder* b, Builder* sub) { /* append sub's nodes; returns its root's index */
+    const uint64_t off = b->n_nodes;
+    for (uint64_t i = 0; i < sub->n_nodes; ++i) {
+        Node nd = sub->nodes[i];
+        if (nd.left >= 0) { nd.left += (int64_t)off; nd.right += (int64_t)off; }
+        push_node(b, nd);
+    }
+    if (sub->max_depth > b->max_depth) b->max_depth = sub->max_depth;
+    free(sub->nodes);
+    return off;
 }
 static void bvh_build(BVH* bvh, const AABB* boxes, uint64_t n, uint64_t* perm_out) {
     bvh->n = n; bvh->nodes = NULL; bvh->n_nodes = 0; bvh->depth = 0;
     for (uint64_t i = 0; i < n; ++i) perm_out[i] = i;
     if (n == 0) return; /* BVH::new(vec![]) builds a leaf over nothing; never traversed (bvh.rs:29) */
-    Builder b = {boxes, perm_out, NULL, 0, 0, NULL, NULL, 0};
-    b.fwd = (AABB*)malloc(sizeof(AABB) * (n > 1 ? n - 1 : 1));
-    b.bwd = (AABB*)malloc(sizeof(AABB) * (n > 1 ? n - 1 : 1));
-    build_nodes(&b, 0, n, 1);
-    free(b.fwd); free(b.bwd);
+    /* the midpoint comparator's keys (bvh.rs:137-140: (min + max) / 2 per axis,
+       f64::total_cmp order), once per primitive instead of per comparison */
+    int64_t* keys = (int64_t*)malloc(sizeof(int64_t) * 3 * n);
+    for (uint64_t i = 0; i < n; ++i)
+        for (int axis = 0; axis < 3; ++axis)
+            keys[axis * n + i] = total_order_key((axis_of(boxes[i].min, axis) + axis_of(boxes[i].max, axis)) / 2.0);
+    Builder root = {boxes, perm_out, NULL, 0, 0, NULL, NULL, 0, {keys, keys + n, keys + 2 * n}};
+    Builder b;
+    if (n >= kParMin) {
+#pragma omp parallel
+#pragma omp single
+        build_sub(&root, 0, n, 1, &b);
+    } else {
+        build_sub(&root, 0, n, 1, &b);
+    }
+    free(keys);
     bvh->nodes = b.nodes; bvh->n_nodes = b.n_nodes; bvh->depth = b.max_depth;
 }
 static void bvh_build_shapes(BVH* bvh, Shape* list, uint64_t n) {

@@ -35,7 +35,7 @@ def _threads():
 
 
 @pytest.mark.parametrize("name,rows", [("C2", [0, 540, 1079]), ("C3", [1, 600])])
-def test_full_frame_rows_match_oracle(rt, orc, monkeypatch, name, rows):
+def test_full_frame_rows_match_oracle(rt, orc, name, rows):
     desc, params = _workload(rt, name)
     scene = rt.Scene(desc)
     img, _, st = scene.generate_image(params, stats=True)
@@ -52,7 +52,8 @@ def test_full_frame_rows_match_oracle(rt, orc, monkeypatch, name, rows):
         assert o_st["paths"] == params.width * params.spp
     if name == "C3":
         # the other segment form renders the identical frame (C3 picks the resumable one)
-        monkeypatch.setenv("RT_RESUME", "0")
+        assert scene.tuning()["resume"] == 1
+        scene.set_tuning(resume=0)
         img2, _, st2 = scene.generate_image(params, stats=True)
         assert np.array_equal(img, img2)
         assert st2["segments"] == st["segments"] and st2["tri_tests"] == st["tri_tests"]

@@ -11,7 +11,7 @@ import pytest
 
 from conftest import REPO
 import gltf_scenes
-from test_gpu_parity import _compare, intersect_device, segment_form  # noqa: F401 (autouse: both segment forms)
+from test_gpu_parity import _compare, form, intersect_device, segment_form  # noqa: F401 (autouse: every form)
 
 pytestmark = pytest.mark.gpu
 
@@ -60,11 +60,10 @@ def test_room_deep_fov(room):
     _compare(g, o, params.replace(width=17, height=23, spp=3, ray_depth=20, fov=1.4, seed=11))
 
 
-@pytest.mark.parametrize("waves", ["3", "4"])
-def test_atrium(atrium, monkeypatch, waves):
-    monkeypatch.setenv("RT_WAVES", waves)
+@pytest.mark.parametrize("waves", [3, 4])
+def test_atrium(atrium, waves):
     desc, params, g, o = atrium
-    img, _, st = _compare(g, o, params)
+    img, _, st = _compare(g, o, params, waves=waves)
     assert st["tri_tests"] > 0 and img.max() > 0
     assert st["lane_steps"] <= st["wave_steps"]
 

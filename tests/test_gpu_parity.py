@@ -30,28 +30,39 @@ def sink(rt, orc, scene_text):
     return desc, params, rt.Scene(desc), orc.OracleScene(desc)
 
 
+# the kernel form the current test runs (segment_form), applied by _compare
+FORM = {}
+
+
 @pytest.fixture(autouse=True, params=["fused", "resume", "resume_eager", "general"])
-def segment_form(request, monkeypatch):
+def segment_form(request):
     """Every test runs both path-kernel segment forms: fused (whole closest-hit
     query, then shading) and resumable (triangle traversal suspended while few
-    lanes are live); the host picks one per scene (RT_RESUME).
+    lanes are live); the host picks one per scene (rt_tuning.resume).
     "resume_eager" suspends whenever any lane waits and tests every leaf at once
-    (RT_SUSPEND_LANES=64, RT_LEAF_LANES=1: the far ends of the per-scene knobs the
+    (suspend_lanes=64, leaf_lanes=1: the far ends of the per-scene knobs the
     host picks, api.cpp path_suspend / path_leaf_batch).
-    "general" is the fused form in its all-kinds instance (RT_KINDS=3) where the
+    "general" is the fused form in its all-kinds instance (kinds=3) where the
     host would pick a shape-only or triangle-only one (api.cpp path_kinds)."""
-    monkeypatch.setenv("RT_RESUME", "1" if request.param.startswith("resume") else "0")
+    FORM.clear()
+    FORM["resume"] = 1 if request.param.startswith("resume") else 0
     if request.param == "resume_eager":
-        monkeypatch.setenv("RT_SUSPEND_LANES", "64")
-        monkeypatch.setenv("RT_LEAF_LANES", "1")
+        FORM.update(suspend_lanes=64, leaf_lanes=1)
     if request.param == "general":
-        monkeypatch.setenv("RT_KINDS", "3")
-    return request.param
+        FORM["kinds"] = 3
+    yield request.param
+    FORM.clear()
 
 
-def _compare(gpu_scene, ora_scene, params):
-    from conftest import load_package
-    _, chunk_spp = load_package().sample_chunks(params)
+def form(scene, **extra):
+    """Apply the current test's kernel form (+ extra fields) to a device scene."""
+    scene.set_tuning(**{**FORM, **extra})
+    return scene
+
+
+def _compare(gpu_scene, ora_scene, params, **tuning):
+    form(gpu_scene, **tuning)
+    _, chunk_spp = gpu_scene.sample_chunks(params)
     g_img, g_hits, g_st = gpu_scene.generate_image(params, hit_ids=True, stats=True)
     o_img, o_hits, o_st = ora_scene.render(params, mode=1, hit_ids=True, chunk_spp=chunk_spp)
     r_img, r_hits, _ = ora_scene.render(params, mode=0, hit_ids=True)
@@ -144,21 +155,22 @@ def test_cornell_small(cornell):
     _compare(g, o, params.replace(width=48, height=40, spp=4))
 
 
-@pytest.mark.parametrize("waves", ["3", "4"])
-def test_both_register_budgets(cornell, monkeypatch, waves):
+@pytest.mark.parametrize("waves", [3, 4])
+def test_both_register_budgets(cornell, waves):
     """Both path-kernel instances (3 and 4 waves/SIMD) are bit-exact (host picks per scene)."""
-    monkeypatch.setenv("RT_WAVES", waves)
     desc, params, g, o = cornell
-    _compare(g, o, params.replace(width=40, height=24, spp=3, seed=3))
+    _compare(g, o, params.replace(width=40, height=24, spp=3, seed=3), waves=waves)
+    assert g.tuning()["waves"] == waves
 
 
-@pytest.mark.parametrize("chunk_spp", ["37", "1"])
-def test_sample_ring_wraps(sink, monkeypatch, chunk_spp):
+@pytest.mark.parametrize("chunk_spp", [37, 1])
+def test_sample_ring_wraps(sink, chunk_spp):
     """Long sample runs: the 8-row commit ring wraps many times (37 + 3 rows per
     wave-tile); run length 1: one row per wave-tile, 40 partials per pixel."""
-    monkeypatch.setenv("RT_CHUNK_SPP", chunk_spp)
     desc, params, g, o = sink
-    _compare(g, o, params.replace(width=20, height=12, spp=40, ray_depth=8, seed=17))
+    p = params.replace(width=20, height=12, spp=40, ray_depth=8, seed=17)
+    _compare(g, o, p, chunk_spp=chunk_spp)
+    assert g.sample_chunks(p) == ((40 + chunk_spp - 1) // chunk_spp, chunk_spp)
 
 
 def test_cornell_seed_changes_image(cornell):

@@ -192,7 +192,7 @@ def test_chunked_sum_is_reassociation_only(rt, orc, scene_text):
 
 @pytest.mark.parametrize("w,h,spp,want", [
     (1920, 1080, 256, (32, 8)),     # C2/C3: 8-spp chunks (66M work units: short wave-tiles trim the 8-GPU tail)
-    (3840, 2160, 1024, (64, 16)),   # C4: 16-spp chunks
+    (3840, 2160, 1024, (16, 64)),   # C4: capped by the 4-GiB partial-sum budget (64 chunks: 12.7 GB)
     (1920, 1080, 64, (16, 4)),      # C5
     (256, 256, 64, (64, 1)),        # C1: capped at kMaxChunks
     (48, 32, 4, (4, 1)),
@@ -204,6 +204,7 @@ def test_sample_chunk_rule(rt, w, h, spp, want):
     k, cs = rt.sample_chunks(rt.RenderParams(w, h, spp))
     assert (k, cs) == want
     assert (k - 1) * cs < spp <= k * cs   # no empty run, all samples covered
+    assert ((w + 15) // 16) * ((h + 15) // 16) * 256 * 3 * 8 * k <= 4 << 30  # partial sums within budget
 
 
 def test_thread_count_independent(rt, orc, scene_text):

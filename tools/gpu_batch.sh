@@ -23,7 +23,7 @@ run() {  # run <name> <seconds> <cmd...>
 }
 for s in $STEPS; do
   case $s in
-    tests) run pytest_gpu 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread || exit 1 ;;
+    tests) run pytest_gpu 1000 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
     bench) run bench_default 900 $B --gpus 1 --steps 20 --warmup 5 || exit 1 ;;
     multi) run pytest_multi 600 python3 -u -m pytest tests/test_gpu_multi.py -m gpu -x -v --timeout 300 \
              --timeout-method thread || exit 1 ;;
@@ -85,6 +85,13 @@ for s in $STEPS; do
         TCP_TOTAL_CACHE_ACCESSES_sum --output-format csv -d "$OUT/tcp_$w" -o run \
         -- $B --workload $w --steps 1 --warmup 0 --no-cpu-baseline --no-pmc ${WAIT_SPP:+--spp $WAIT_SPP} || exit 1 ;;
     share2) run share_C2 600 python3 tools/share_scaling.py C2 256 1 8 || exit 1 ;;
+    share4) run share_C4 900 python3 tools/share_scaling.py C4 1024 1 8 || exit 1 ;;
+    smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
+    c4)    run bench_c4 900 $B --workload C4 --steps 2 --warmup 1 || exit 1 ;;
+    prof4) run prof_c4 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c4" -o run \
+             -- $B --workload C4 --steps 2 --warmup 1 --no-cpu-baseline --no-pmc || exit 1 ;;
+    prof5) run prof_c5 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c5" -o run \
+             -- $B --workload C5 --steps 2 --warmup 1 --no-cpu-baseline --no-pmc || exit 1 ;;
     var5)  run variants_C5 900 python3 tools/variants.py C5 ${VAR_SPP5:-16} \
              ${VARIANTS:-cpu-raytracing-rt_amd/build*/librt_amd.so} || exit 1 ;;
     *) echo "unknown step $s"; exit 2 ;;

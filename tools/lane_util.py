@@ -1,6 +1,6 @@
 """Lane utilisation of the path-regeneration loop vs sample-run length.
 usage: python tools/lane_util.py WORKLOAD [SPP] [chunk_spp ...]
-Per chunk length (RT_CHUNK_SPP override): kernel ms of a plain render and
+Per chunk length (rt_tuning.chunk_spp): kernel ms of a plain render and
 lane_steps / wave_steps from a stats render (fraction of SIMD lane-steps doing
 path work; the rest is lanes idling at the end of their wave's run)."""
 import json
@@ -23,10 +23,10 @@ chunks = [int(x) for x in sys.argv[3:]] or [spp, 64, 32, 16, 8]
 desc, params = bench.load_workload(rt, scene_file, W, H, spp)
 scene = rt.Scene(desc)
 for cs in chunks:
-    os.environ["RT_CHUNK_SPP"] = str(cs)
+    scene.set_tuning(chunk_spp=cs)
     _, _, st = scene.generate_image(params, stats=True)
     ms = min(scene.generate_image(params)[2]["kernel_ms"] for _ in range(2))
-    print(json.dumps({"workload": wl, "spp": spp, "chunk_spp": cs, "chunks": rt.sample_chunks(params)[0],
+    print(json.dumps({"workload": wl, "spp": spp, "chunk_spp": cs, "chunks": scene.sample_chunks(params)[0],
                       "kernel_ms": ms, "Mseg_s": st["segments"] / ms / 1e3,
                       "lane_util": st["lane_steps"] / max(1, st["wave_steps"]), "segments": st["segments"]}),
           flush=True)

@@ -1,7 +1,8 @@
 """Per-rank render time of a strong-scaled frame on ONE GPU: rank r's tile share
 of an N-way partition (rt_render_tiles_async), timed alone with HIP events, for
-each N and rank.  The slowest share x N over the N=1 frame is the render-side
-strong-scaling efficiency the 8-GPU bench can reach (no gather or launch cost).
+each N and EVERY rank (median of 3 timed runs after a warm one).  The slowest
+share x N over the N=1 frame is the render-side strong-scaling efficiency the
+N-GPU bench can reach (no gather or launch cost).
 usage: python tools/share_scaling.py [WORKLOAD] [SPP] [N ...]"""
 import json
 import os
@@ -33,22 +34,23 @@ for n in ns:
     per = scene.tiles_per_rank(params, n)
     tiles = torch.empty((per, 256, 3), dtype=torch.float64, device=dev)
     times = []
-    for rank in (range(n) if n <= 2 else (0, n // 2, n - 1)):
+    runs = []
+    for rank in range(n):
         scene.render_tiles_async(params, rank, n, tiles.data_ptr(), stream.cuda_stream)  # warm
-        best = None
+        ms = []
         for _ in range(3):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             scene.render_tiles_async(params, rank, n, tiles.data_ptr(), stream.cuda_stream)
             e1.record(stream)
             torch.cuda.synchronize()
-            ms = e0.elapsed_time(e1)
-            best = ms if best is None else min(best, ms)
-        times.append(best)
+            ms.append(e0.elapsed_time(e1))
+        runs.append(ms)
+        times.append(float(sorted(ms)[1]))  # median of 3
     worst = max(times)
     if n == 1:
         t1 = worst
-    out["ms"][n] = {"per_rank": times, "worst": worst,
+    out["ms"][n] = {"per_rank_median": times, "per_rank_runs": runs, "worst": worst,
                     "efficiency": (t1 / (n * worst)) if t1 else None}
     print(json.dumps({n: out["ms"][n]}), flush=True)
 print(json.dumps(out))

@@ -1,7 +1,7 @@
 """Time alternate builds of librt_amd.so on a bench workload at reduced spp.
 usage: python tools/variants.py WORKLOAD SPP lib1.so lib2.so[@VAR=val,VAR2=val] ...   (each in its own process)
-WORKLOAD is a bench.py workload name (C1, C2, C3, ...); `@VAR=val,...` sets environment overrides
-(e.g. RT_WAVES=3, RT_RESUME=0) for that run."""
+WORKLOAD is a bench.py workload name (C1, C2, C3, ...); `@field=val,...` forces rt_tuning fields
+(e.g. waves=3,resume=0,suspend_lanes=32) for that run (Scene.set_tuning)."""
 import os
 import subprocess
 import sys
@@ -20,12 +20,14 @@ desc, params = bench.load_workload(rt, scene_file, W, H, int(sys.argv[3]))
 if depth:
     params = params.replace(ray_depth=depth)
 s = rt.Scene(desc)
+tune = {k: int(v) for k, v in (kv.split("=", 1) for kv in os.environ.get("RT_VARIANT_ENV", "").split(",") if kv)}
+s.set_tuning(**tune)
 _, _, st = s.generate_image(params, stats=True)
 ks = []
 for i in range(3):
     _, _, st2 = s.generate_image(params)
     ks.append(st2["kernel_ms"])
-print(json.dumps({"lib": os.environ["RT_AMD_LIB"], "env": os.environ.get("RT_VARIANT_ENV", ""), "workload": sys.argv[2], "spp": params.spp, "kernel_ms": ks,
+print(json.dumps({"lib": os.environ["RT_AMD_LIB"], "tuning": s.tuning(), "workload": sys.argv[2], "spp": params.spp, "kernel_ms": ks,
                   "Mseg_s": st["segments"] / min(ks) / 1e3, "segments": st["segments"]}))
 '''
 wl, spp = sys.argv[1], sys.argv[2]
@@ -33,7 +35,6 @@ rc = 0
 for arg in sys.argv[3:]:
     lib, _, over = arg.partition("@")
     env = dict(os.environ, RT_AMD_LIB=os.path.abspath(lib), RT_VARIANT_ENV=over)
-    env.update(kv.split("=", 1) for kv in over.split(",") if kv)
     r = subprocess.run([sys.executable, "-c", CHILD, os.path.dirname(HERE), wl, spp], env=env, capture_output=True,
                        text=True, timeout=600)
     print(r.stdout.strip() or r.stderr[-2000:], flush=True)
