@@ -1034,13 +1034,11 @@ RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, P
     const DevMaterial& m = S.mats[mat];
     const V3 col = load3(m.color);
     ps.L = ps.L + mul(ps.T, load3(m.emission));
-    // On the last segment the rest of the shading (direction, light pdf, weight)
-    // only feeds raytrace_impl(left - 1) == 0: a throughput nothing reads again and
-    // draws no later segment makes.  The product stops here (the radiance and hit
-    // ids are the same bits); the stats build (ST) still runs it, so the work
-    // counters stay the oracle's (whose light query on the last bounce the SURVEY
-    // byte model counts).
-#ifndef RT_NO_LASTSEG  // ablation build: the last segment shades like every other
+    // The last segment shades like every other: its direction and pdf decide
+    // whether raytrace_impl's last level is NaN (below).  RT_LASTSEG_SHORTCUT is the
+    // round-2 form that stopped after the emission (C2 -2.6% at 64 spp, but it
+    // misses that NaN, so it is an ablation build only).
+#ifdef RT_LASTSEG_SHORTCUT
     if (!ST && last) return false;
 #endif
     rng_align(rng);   // shading draws start on a block boundary (oracle.c rng_align)
@@ -1092,6 +1090,11 @@ RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, P
         double pdf = empty ? cp : (cp + lp) / 2.0;  // Mix::pdf
         if (pdf == 0.0) return false;
         ps.T = mul(ps.T, diffuse_weight(col, cp, pdf));
+        // The last bounce: raytrace_impl still adds dot * col (x) raytrace_impl(.., 0) / pi
+        // / pdf (raytrace.rs:13,32-33), NaN exactly when the direction or the pdf is NaN
+        // (a NaN light pdf is reachable: oracle.c raytrace_iter); it reaches the pixel
+        // through every enclosing level.  T is not read again, so the rule is explicit.
+        if (last && (isnan(cs) || isnan(pdf))) ps.L = v3(NAN, NAN, NAN);
         ps.o = pos + dir * kEpsilon;
         ps.d = dir;
         return true;
@@ -1134,7 +1137,7 @@ RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, P
 // the resumable form's end of a segment: finish `intersect`, then shade
 template <bool ST, int KM = 3, class Stk>
 RT_D bool segment_end(const DevScene& S, const KParams& P, const Scales& sc, PathState& ps, Rng& rng,
-                      Stk& stk, Cnt<ST>& C, SegQuery& q, int32_t& hit_gid) {
+                      Stk& stk, Cnt<ST>& C, SegQuery& q, int32_t& hit_gid, bool last) {
     Hit h; uint32_t mat = 0; int32_t gid = 0;
     if (KM == kTris) {  // the candidate is the triangle traversal's (take_tri on an empty best)
         q.best.valid = false; q.best.t = 0.0; q.best.u = q.best.v = 0.0; q.best.prim = 0; q.best.aux = 0;
@@ -1142,9 +1145,7 @@ RT_D bool segment_end(const DevScene& S, const KParams& P, const Scales& sc, Pat
     }
     take_tri(q.best, q.T.valid, q.T.best, q.T.bu, q.T.bv, q.T.prim);
     const bool hit = intersect_tail<ST, KM>(S, q.best, ps.o, ps.d, C, h, mat, gid);
-    // (no last-segment shortcut here: it cost the 4-wave resumable kernel's
-    // register allocation more than it saved, C3 +1.5%)
-    return segment_shade<ST, Stk, false, KM>(S, P, sc, ps, rng, stk, C, hit, h, mat, gid, hit_gid, false, false);
+    return segment_shade<ST, Stk, false, KM>(S, P, sc, ps, rng, stk, C, hit, h, mat, gid, hit_gid, false, last);
 }
 
 // the fused form: one whole segment (scene_intersect to completion, then shade)
@@ -1449,7 +1450,7 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
                 if (inq) {
                     int32_t g;
                     const unsigned long long ph_s = PH_T();
-                    cont = segment_end<ST, KM>(S, P, sc, ps, rng, stk, C, q, g);
+                    cont = segment_end<ST, KM>(S, P, sc, ps, rng, stk, C, q, g, b + 1 >= depth);
                     PH_ADDW(kPhSegment, ph_s);
                     if (HIT) hit_ids[(pixel * P.spp + s) * depth + b] = g;
                     ++b;

@@ -954,6 +954,66 @@ static V3 light_sample(const oracle_scene* s, V3 pos, uint64_t A, uint64_t B, ui
 }
 static inline int lights_empty(const oracle_scene* s) { return s->lells.n == 0 && s->lboxes.n == 0 && s->ltris.n == 0; }
 
+/* ---- literal draws (mode 2) -------------------------------------------- */
+/* The reference's own sequence of rand 0.8.5 calls per diffuse bounce, on the
+   same Philox word stream, with none of this build's layout choices (no block
+   alignment at hits, no shared A/B/C draws, no exact UniformInt zone, an index
+   draw even for one light).  Used only to pin, statistically, that the build's
+   layout (modes 0/1, the device's) is the same estimator
+   (tests/test_oracle.py::test_layout_matches_literal_draw_order). */
+static int gen_bool_half_ref(Rng* r) { /* rng.gen_bool(0.5) (ray_sampler.rs:88): Bernoulli p_int = 2^63 */
+    return next_u64(r) < 0x8000000000000000ull;
+}
+static uint64_t gen_range_usize_ref(Rng* r, uint64_t n) {
+    /* rng.gen_range(0..n) (ray_sampler.rs:102): UniformInt<usize>::sample_single_inclusive(0, n-1)
+       with rand's conservative zone (range << leading_zeros) - 1 for types wider than u16 */
+    const uint64_t range = n, zone = (range << __builtin_clzll(range)) - 1;
+    for (;;) {
+        uint64_t v = next_u64(r);
+        unsigned __int128 m = (unsigned __int128)v * range;
+        if ((uint64_t)m <= zone) return (uint64_t)(m >> 64);
+    }
+}
+static int32_t gen_range_i32_incl_ref(Rng* r, int32_t low, int32_t high) {
+    /* rng.gen_range(0..=1) (ray_sampler.rs:147, an i32 literal): UniformInt<i32> draws u32
+       words, conservative zone */
+    const uint32_t range = (uint32_t)(high - low) + 1u, zone = (range << __builtin_clz(range)) - 1u;
+    for (;;) {
+        uint64_t m = (uint64_t)next_u32(r) * range;
+        if ((uint32_t)m <= zone) return low + (int32_t)(uint32_t)(m >> 32);
+    }
+}
+static V3 uniform_on_box_ref(V3 s, Rng* r) { /* ray_sampler.rs:142-157, call for call */
+    double w4x = s.y * s.z, w4y = s.x * s.z, w4z = s.x * s.y;
+    double choice = gen_range_f64(r, 0.0, (w4x + w4y) + w4z);
+    double sign = (double)(gen_range_i32_incl_ref(r, 0, 1) * 2 - 1);
+    double u1 = gen_range_incl_f64(r, -1.0, 1.0);
+    double u2 = gen_range_incl_f64(r, -1.0, 1.0);
+    V3 p;
+    if (choice < w4x) p = v3(sign, u1, u2);
+    else if (choice < w4x + w4y) p = v3(u1, sign, u2);
+    else p = v3(u1, u2, sign);
+    return vmul(p, s);
+}
+static V3 light_sample_ref(const oracle_scene* s, V3 pos, Rng* r) { /* ray_sampler.rs:101-130, call for call */
+    uint64_t index = gen_range_usize_ref(r, s->lells.n + s->lboxes.n + s->ltris.n);
+    V3 world;
+    if (index < s->lboxes.n) {
+        const Shape* l = &s->lboxes.s[index];
+        world = vadd(qrot(l->rot, uniform_on_box_ref(l->shape, r)), l->pos);
+    } else if (index < s->lboxes.n + s->lells.n) {
+        const Shape* l = &s->lells.s[index - s->lboxes.n];
+        world = vadd(qrot(l->rot, vmul(uniform_on_sphere(r), l->shape)), l->pos);
+    } else {
+        const Triangle* t = &s->ltris.t[index - s->lboxes.n - s->lells.n].tri;
+        double u = gen_range_incl_f64(r, 0.0, 1.0);
+        double v = gen_range_incl_f64(r, 0.0, 1.0);
+        if (u + v > 1.0) { u = 1.0 - u; v = 1.0 - v; }
+        world = vadd(vadd(vscale(t->ba, u), vscale(t->ca, v)), t->a);
+    }
+    return vnormalize(vsub(world, pos));
+}
+
 /* ======================================================================= */
 /* raytrace.rs                                                              */
 /* ======================================================================= */
@@ -963,6 +1023,7 @@ static inline double powi5(double x) { double x2 = x * x; return x * (x2 * x2); 
 typedef struct {
     const oracle_scene* s; const rt_render_params* p; Rng* rng; Counters* c;
     int32_t* hits; /* [ray_depth] for this (pixel, sample) or NULL */
+    int literal;   /* mode 2: the reference's own rand call sequence (see "literal draws") */
 } Ctx;
 
 static inline void reflected_ray(V3 o, V3 d, const Hit* h, V3* ro, V3* rd) { /* raytrace.rs:67-73 */
@@ -997,6 +1058,8 @@ static int diffuse_sample(Ctx* x, V3 pos, V3 n, V3* dir_out, double* pdf_out) {
     V3 dir;
     int empty = lights_empty(s);
     if (empty) dir = cosine_sample(n, x->rng);
+    else if (x->literal) /* Mix::sample :87-93 as written: coin, then the chosen sampler's own draws */
+        dir = gen_bool_half_ref(x->rng) ? cosine_sample(n, x->rng) : light_sample_ref(s, pos, x->rng);
     else { /* Mix::sample :87-93, with the shared draws A, B, C (see uniform_on_box) */
         int coin = gen_half(x->rng);
         uint64_t A = next_u64(x->rng), B = next_u64(x->rng), C = next_u64(x->rng);
@@ -1018,7 +1081,7 @@ static V3 raytrace_impl(Ctx* x, V3 o, V3 d, uint32_t left) { /* raytrace.rs:12-6
     int hit = scene_intersect(x->s, o, d, &sh, x->c);
     if (x->hits) x->hits[bounce] = hit ? (int32_t)sh.gid : RT_HIT_MISS;
     if (!hit) return vld(x->p->bg_color);
-    rng_align(x->rng);
+    if (!x->literal) rng_align(x->rng);
     const rt_material* m = &x->s->mats[sh.mat];
     const Hit* h = &sh.h;
     V3 e = vld(m->emission), col = vld(m->color);
@@ -1079,6 +1142,13 @@ static V3 raytrace_iter(Ctx* x, V3 o, V3 d) {
             double f = cosine_pdf(h->ns, dir) / pdf;
             V3 w = v3(col.x * f, col.y * f, col.z * f);
             T = vmul(T, w);
+            /* The last bounce: the recursive form still evaluates dot * col (x) 0 / pi / pdf
+               with raytrace_impl(.., 0) == 0 (raytrace.rs:13,32-33), which is NaN exactly
+               when the direction or the pdf is NaN (e.g. a NaN light pdf: a query ray that
+               starts inside a rotated light box by rounding, t^2/|d.n| = 0/0); the NaN then
+               reaches the pixel through every enclosing level.  T is not read again here,
+               so the rule is explicit. */
+            if (b + 1 == depth && (isnan(vdot(dir, h->ns)) || isnan(pdf))) { L = v3(NAN, NAN, NAN); break; }
             o = vadd(pos, vscale(dir, R_EPSILON));
             d = dir;
         } else if (m->kind == RT_MAT_DIELECTRIC) {
@@ -1140,10 +1210,10 @@ int oracle_render(const oracle_scene* s, const rt_render_params* p, int mode, in
     return oracle_render_chunked(s, p, mode, threads, row_begin, row_end, 0, out, hit_ids, stats);
 }
 
-int oracle_render_chunked(const oracle_scene* s, const rt_render_params* p, int mode, int threads,
-                          uint32_t row_begin, uint32_t row_end, uint32_t chunk_spp,
-                          double* out, int32_t* hit_ids, rt_stats* stats) {
-    if (!s || !p || !out || p->width == 0 || p->height == 0) return RT_ERR_INVALID;
+static int render_impl(const oracle_scene* s, const rt_render_params* p, int mode, int threads,
+                       uint32_t row_begin, uint32_t row_end, uint32_t chunk_spp,
+                       double* out, double* out_sq, int32_t* hit_ids, rt_stats* stats) {
+    if (!s || !p || !out || p->width == 0 || p->height == 0 || mode < 0 || mode > 2) return RT_ERR_INVALID;
     if (chunk_spp == 0 || chunk_spp > p->spp) chunk_spp = p->spp;
     if (row_end > p->height) row_end = p->height;
     if (row_begin >= row_end) return RT_ERR_INVALID;
@@ -1165,25 +1235,27 @@ int oracle_render_chunked(const oracle_scene* s, const rt_render_params* p, int 
 #endif
         Counters* c = &tc[tid];
         uint32_t x = (uint32_t)(idx % W), y = (uint32_t)(idx / W);
-        V3 sum = v3(0, 0, 0), run = v3(0, 0, 0);
+        V3 sum = v3(0, 0, 0), run = v3(0, 0, 0), sq = v3(0, 0, 0);
         for (uint32_t smp = 0; smp < spp; ++smp) {
             Rng rng;
             rng_init(&rng, p->seed, idx, smp);
             int32_t* hrow = hit_ids ? hit_ids + (idx * spp + smp) * depth : NULL;
             if (hrow) for (uint32_t b = 0; b < depth; ++b) hrow[b] = RT_HIT_NONE;
-            Ctx cx = {s, p, &rng, c, hrow};
+            Ctx cx = {s, p, &rng, c, hrow, mode == 2};
             V3 o, d;
             fuzzy_ray(&cam, x, y, &rng, &o, &d);
             d = vnormalize(d); /* raytrace.rs:9 */
             c->paths++;
-            V3 L = mode == 0 ? raytrace_impl(&cx, o, d, depth) : raytrace_iter(&cx, o, d);
+            V3 L = mode == 1 ? raytrace_iter(&cx, o, d) : raytrace_impl(&cx, o, d, depth);
             run = vadd(run, L);
+            if (out_sq) sq = vadd(sq, vmul(L, L));
             if ((smp + 1) % chunk_spp == 0 || smp + 1 == spp) { /* end of a run (one run = main.rs's sum) */
                 sum = smp < chunk_spp ? run : vadd(sum, run);
                 run = v3(0, 0, 0);
             }
         }
         vst(out + 3 * idx, vdivs(sum, (double)spp)); /* main.rs:104 before tonemapping */
+        if (out_sq) vst(out_sq + 3 * idx, vdivs(sq, (double)spp));
     }
     if (stats) {
         memset(stats, 0, sizeof(*stats));
@@ -1196,6 +1268,18 @@ int oracle_render_chunked(const oracle_scene* s, const rt_render_params* p, int 
     }
     free(tc);
     return 0;
+}
+
+int oracle_render_chunked(const oracle_scene* s, const rt_render_params* p, int mode, int threads,
+                          uint32_t row_begin, uint32_t row_end, uint32_t chunk_spp,
+                          double* out, int32_t* hit_ids, rt_stats* stats) {
+    return render_impl(s, p, mode, threads, row_begin, row_end, chunk_spp, out, NULL, hit_ids, stats);
+}
+
+int oracle_render_moments(const oracle_scene* s, const rt_render_params* p, int mode, int threads,
+                          uint32_t row_begin, uint32_t row_end, double* out_mean, double* out_sq, rt_stats* stats) {
+    if (!out_sq) return RT_ERR_INVALID;
+    return render_impl(s, p, mode, threads, row_begin, row_end, 0, out_mean, out_sq, NULL, stats);
 }
 
 void oracle_intersect_rays(const oracle_scene* s, const double* rays, uint32_t n, rt_hit* out) {

@@ -40,7 +40,12 @@ int64_t oracle_scene_bvh_prim(const oracle_scene* s, int k, uint64_t i);
 
 /* generate_image (main.rs:85-114) without tonemapping: mean radiance.
    mode 0 = recursive raytrace_impl (raytrace.rs:12-60, faithful form),
-   mode 1 = iterative throughput form (the device algorithm, bit-identical to it).
+   mode 1 = iterative throughput form (the device algorithm, bit-identical to it),
+   mode 2 = recursive raytrace_impl drawing the reference's own rand 0.8.5 call
+            sequence (ray_sampler.rs:87-157, raytrace.rs:46: gen_bool(0.5) coin,
+            per-branch draws, an index draw even for one light, rand's conservative
+            UniformInt zones, no block alignment) on the same Philox word stream —
+            the statistical pin of the build's stream layout (modes 0/1).
    row_begin/row_end restrict the rendered rows (CPU-baseline sub-window);
    threads <= 0 => OpenMP default.  Returns 0 or negative on error. */
 int oracle_render(const oracle_scene* s, const rt_render_params* p, int mode,
@@ -54,6 +59,13 @@ int oracle_render(const oracle_scene* s, const rt_render_params* p, int mode,
 int oracle_render_chunked(const oracle_scene* s, const rt_render_params* p, int mode,
                           int threads, uint32_t row_begin, uint32_t row_end, uint32_t chunk_spp,
                           double* out_mean_rgb, int32_t* opt_hit_ids, rt_stats* opt_stats);
+
+/* As oracle_render (sequential sum), plus the per-pixel second moment
+   out_sq = sum over samples of L*L / spp per channel (the sample variance of the
+   estimator is out_sq - mean^2). */
+int oracle_render_moments(const oracle_scene* s, const rt_render_params* p, int mode,
+                          int threads, uint32_t row_begin, uint32_t row_end,
+                          double* out_mean_rgb, double* out_sq, rt_stats* opt_stats);
 
 /* intersect(ray, primitives, +inf) for a batch (intersections.rs:42-62). */
 void oracle_intersect_rays(const oracle_scene* s, const double* rays, uint32_t n, rt_hit* out);

@@ -38,6 +38,7 @@ def lib():
             "oracle_scene_bvh_prim": (C.c_int64, [vp, i32, u64]),
             "oracle_render": (i32, [vp, vp, i32, i32, u32, u32, vp, vp, vp]),
             "oracle_render_chunked": (i32, [vp, vp, i32, i32, u32, u32, u32, vp, vp, vp]),
+            "oracle_render_moments": (i32, [vp, vp, i32, i32, u32, u32, vp, vp, vp]),
             "oracle_intersect_rays": (None, [vp, vp, u32, vp]),
             "oracle_light_pdf_rays": (None, [vp, vp, u32, vp]),
             "oracle_aabb_intersects": (i32, [dp, dp, dp, dp, dp]),
@@ -106,7 +107,8 @@ class OracleScene:
 
     def render(self, params, mode: int = 1, threads: int = 0, rows=None, hit_ids: bool = False,
                chunk_spp: int = 0):
-        """generate_image without tonemapping. mode 0 = recursive, 1 = iterative (device algorithm).
+        """generate_image without tonemapping. mode 0 = recursive, 1 = iterative (device algorithm),
+        2 = recursive with the reference's literal rand call sequence.
         chunk_spp > 0 sums samples in runs of chunk_spp like the device's chunked
         work units (oracle_render_chunked); 0 = the reference's sequential sum.
         Returns (image [H, W, 3], hit ids or None, stats dict)."""
@@ -123,6 +125,19 @@ class OracleScene:
         if rc != 0:
             raise RuntimeError(f"oracle_render failed: {rc}")
         return img, hits, {k: getattr(st, k) for k, _ in st._fields_}
+
+    def render_moments(self, params, mode: int = 0, threads: int = 0):
+        """(mean [H, W, 3], second moment [H, W, 3], stats): mode 0 = the build's stream
+        layout (recursive form), 2 = the reference's literal rand call sequence."""
+        H, W = params.height, params.width
+        mean = np.zeros((H, W, 3), np.float64)
+        sq = np.zeros((H, W, 3), np.float64)
+        st = _stats_struct()
+        rc = lib().oracle_render_moments(self._h, C.byref(params.to_c()), mode, threads, 0, H, mean.ctypes.data,
+                                         sq.ctypes.data, C.byref(st))
+        if rc != 0:
+            raise RuntimeError(f"oracle_render_moments failed: {rc}")
+        return mean, sq, {k: getattr(st, k) for k, _ in st._fields_}
 
     def intersect(self, rays):
         from importlib import import_module  # noqa: F401

@@ -68,13 +68,14 @@ def _compare(gpu_scene, ora_scene, params, **tuning):
     r_img, r_hits, _ = ora_scene.render(params, mode=0, hit_ids=True)
     assert np.array_equal(g_hits, o_hits), f"hit ids differ at {np.argwhere(g_hits != o_hits)[:5]}"
     assert np.array_equal(g_hits, r_hits)
-    assert np.array_equal(g_img, o_img), f"max |d| {np.max(np.abs(g_img - o_img))}"
+    # NaN pixels (a NaN light pdf is reachable, test_last_bounce_nan) must sit in the same places
+    assert np.array_equal(g_img, o_img, equal_nan=True), f"max |d| {np.nanmax(np.abs(g_img - o_img))}"
     # the product instances (no stats: the timed kernel, and hit ids without stats)
     p_img, p_hits, _ = gpu_scene.generate_image(params, hit_ids=True)
-    assert np.array_equal(p_hits, o_hits) and np.array_equal(p_img, o_img)
+    assert np.array_equal(p_hits, o_hits) and np.array_equal(p_img, o_img, equal_nan=True)
     p_img, _, _ = gpu_scene.generate_image(params)
-    assert np.array_equal(p_img, o_img), f"product kernel: max |d| {np.max(np.abs(p_img - o_img))}"
-    np.testing.assert_allclose(g_img, r_img, rtol=REL_TOL, atol=1e-300)
+    assert np.array_equal(p_img, o_img, equal_nan=True), f"product kernel: max |d| {np.nanmax(np.abs(p_img - o_img))}"
+    np.testing.assert_allclose(g_img, r_img, rtol=REL_TOL, atol=1e-300)  # equal_nan: the recursive form's NaNs
     for k in ("paths", "segments", "aabb_tests", "tri_tests", "shape_tests", "shaded_hits",
               "light_queries", "light_hits"):
         assert g_st[k] == o_st[k], (k, g_st[k], o_st[k])
@@ -216,6 +217,20 @@ def test_shared_light_tests_box_lights(box_lights, over):
 def test_no_shared_light_tests_with_other_lights(sink):
     desc, params, g, o = sink
     assert g.info()["shared_light_mask"] == 0  # ellipsoid and triangle lights: separate queries
+
+
+@pytest.mark.parametrize("depth", [3, 6])
+def test_last_bounce_nan(sink, depth):
+    """Pixel 33, sample 213 of the kitchen sink: the second bounce on the rotated light
+    box has a NaN Light::pdf (its query ray starts inside the box by rounding; t^2/|d.n|
+    = NaN, as the reference computes it).  At depth 3 that bounce is the LAST one:
+    raytrace_impl's dot * col (x) 0 / pi / pdf is still NaN (raytrace.rs:32-33), so the
+    pixel is NaN — the timed kernel shades the last segment like every other and applies
+    that rule (render.hip segment_shade), bit-exact with the oracle incl. NaN places."""
+    desc, params, g, o = sink
+    p = params.replace(width=32, height=24, spp=214, ray_depth=depth)
+    img, _, _ = _compare(g, o, p)
+    assert np.isnan(img[1, 1]).all() and np.isnan(img).sum() == 3
 
 
 def test_kitchen_sink_deep(sink):
