@@ -99,15 +99,17 @@ class rt_scene_info(C.Structure):
                 ("n_triangles", C.c_uint64), ("n_light_boxes", C.c_uint32), ("n_light_ellipsoids", C.c_uint32),
                 ("n_light_triangles", C.c_uint64), ("bvh_nodes", C.c_uint64 * 6), ("bvh_depth", C.c_uint32 * 6),
                 ("build_ms", C.c_double), ("upload_ms", C.c_double), ("device_bytes", C.c_uint64),
-                ("shared_light_mask", C.c_uint32), ("reserved", C.c_uint32)]
+                ("shared_light_mask", C.c_uint32), ("layout_flags", C.c_uint32)]
 
 
 class rt_tuning(C.Structure):
     _fields_ = [("waves", C.c_uint32), ("resume", C.c_int32), ("kinds", C.c_uint32),
-                ("suspend_lanes", C.c_uint32), ("leaf_lanes", C.c_uint32), ("chunk_spp", C.c_uint32)]
+                ("suspend_lanes", C.c_uint32), ("leaf_lanes", C.c_uint32), ("chunk_spp", C.c_uint32),
+                ("compact", C.c_int32), ("_reserved", C.c_uint32)]
 
 
-TUNING_AUTO = dict(waves=0, resume=-1, kinds=0, suspend_lanes=0, leaf_lanes=0, chunk_spp=0)
+TUNING_AUTO = dict(waves=0, resume=-1, kinds=0, suspend_lanes=0, leaf_lanes=0, chunk_spp=0, compact=-1)
+RT_LAYOUT_COMPACT_TRIS = 0x1
 
 
 # every symbol include/rt_api.h declares (checked by tests/test_abi.py)
@@ -379,7 +381,8 @@ class Scene:
     def set_tuning(self, **kw):
         """Force the kernel form of this scene's renders (rt_scene_set_tuning): waves (3|4),
         resume (0|1), kinds (3 = all-kinds instance), suspend_lanes, leaf_lanes (1..64),
-        chunk_spp.  Fields not given are auto (the library's per-scene pick)."""
+        chunk_spp, compact (0 = f64 triangle-BVH layout, 1 = compact when the scene has it).
+        Fields not given are auto (the library's per-scene pick)."""
         bad = set(kw) - set(TUNING_AUTO)
         if bad:
             raise ValueError(f"unknown tuning fields {sorted(bad)}")
@@ -390,7 +393,7 @@ class Scene:
         """The resolved kernel form the next render runs (rt_scene_get_tuning)."""
         t = rt_tuning()
         _check(lib().rt_scene_get_tuning(self._h, C.byref(t)))
-        return {k: getattr(t, k) for k, _ in t._fields_}
+        return {k: getattr(t, k) for k, _ in t._fields_ if not k.startswith("_")}
 
     def sample_chunks(self, params: RenderParams):
         """(chunks, chunk_spp) this scene's renders use (rt_scene_sample_chunks)."""

@@ -66,7 +66,7 @@ struct rt_scene {
     // streams never overlap on the shared workspace.
     hipEvent_t ws_done = nullptr;
     // requested kernel form (rt_scene_set_tuning); auto fields resolve per scene
-    rt_tuning tune{0, -1, 0, 0, 0, 0};
+    rt_tuning tune{0, -1, 0, 0, 0, 0, -1, 0};
 };
 
 namespace {
@@ -99,6 +99,8 @@ int upload_bvh(rt_scene* s, const HostBvhArrays& h, DevBvh& d) {
     if ((rc = upload(s, h.tri_inv_area, &d.tri_inv_area))) return rc;
     if ((rc = upload(s, h.mat, &d.mat))) return rc;
     if ((rc = upload(s, h.gid, &d.gid))) return rc;
+    if ((rc = upload(s, h.cnodes, &d.cnodes))) return rc;
+    if ((rc = upload(s, h.ctris, &d.ctris))) return rc;
     return RT_OK;
 }
 
@@ -283,6 +285,15 @@ int path_kinds(const rt_scene* s) {
     return shapes == tris ? 3 : (shapes ? 1 : 2);
 }
 
+// The triangle BVH's compact layout (rt_layout.h DevNodeC, half the bytes per
+// node visit and triangle test, the same numbers): used by the triangle-only
+// 4-wave resumable instance — the kernel of every deep glTF scene — whenever the
+// host could build it (every coordinate an exact f32).  rt_tuning.compact = 0
+// keeps the f64 layout (tests run both).
+bool path_compact(const rt_scene* s) {
+    return s->tune.compact != 0 && s->dev.tris.cnodes && path_waves(s) == 4 && path_resume(s) && path_kinds(s) == 2;
+}
+
 // Suspend threshold of the resumable traversal (render.h kSuspendCached /
 // kSuspendStreamed): by whether the triangle BVH and its hot records fit the
 // Infinity Cache.  rt_tuning.suspend_lanes forces one (tuning).
@@ -313,7 +324,7 @@ int prepare_path(rt_scene* s, KParams& k, bool stats, bool hits, PathWork& W) {
     std::memset(&W, 0, sizeof(W));
     W.waves = path_waves(s);
     W.resume = path_resume(s);
-    W.kinds = path_kinds(s);
+    W.kinds = path_compact(s) ? kKindsCompact : path_kinds(s);
     HIP_TRY(path_grid(stats, hits, W.waves, W.resume, W.kinds, (uint32_t)n_units, &W.grid));
     int rc;
     if ((rc = ensure_spill(s, (uint64_t)W.grid * 64)) || (rc = ensure_part(s, k))) return rc;
@@ -464,6 +475,7 @@ int scene_upload(const HostScene& hs, rt_scene** out) {
     s->info.n_light_ellipsoids = d.lells.n_prims;
     s->info.n_light_triangles = d.ltris.n_prims;
     s->info.shared_light_mask = d.slt_mask;
+    s->info.layout_flags = d.tris.cnodes ? RT_LAYOUT_COMPACT_TRIS : 0u;
     s->info.build_ms = hs.build_ms;
     s->info.upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     *out = owner.release();
@@ -508,11 +520,12 @@ int rt_scene_sample_chunks(const rt_scene* s, const rt_render_params* p, uint32_
 
 int rt_scene_set_tuning(rt_scene* s, const rt_tuning* t) {
     if (!s) return set_error(RT_ERR_INVALID, "scene is NULL");
-    if (!t) { s->tune = rt_tuning{0, -1, 0, 0, 0, 0}; return RT_OK; }
+    if (!t) { s->tune = rt_tuning{0, -1, 0, 0, 0, 0, -1, 0}; return RT_OK; }
     if (t->waves != 0 && t->waves != 3 && t->waves != 4) return set_error(RT_ERR_INVALID, "waves must be 0, 3 or 4");
     if (t->resume < -1 || t->resume > 1) return set_error(RT_ERR_INVALID, "resume must be -1, 0 or 1");
     if (t->kinds != 0 && t->kinds != 3) return set_error(RT_ERR_INVALID, "kinds must be 0 or 3");
     if (t->suspend_lanes > 64 || t->leaf_lanes > 64) return set_error(RT_ERR_INVALID, "lane counts must be <= 64");
+    if (t->compact < -1 || t->compact > 1) return set_error(RT_ERR_INVALID, "compact must be -1, 0 or 1");
     s->tune = *t;
     return RT_OK;
 }
@@ -525,6 +538,8 @@ int rt_scene_get_tuning(const rt_scene* s, rt_tuning* out) {
     out->suspend_lanes = path_suspend(s);
     out->leaf_lanes = path_leaf_batch(s);
     out->chunk_spp = s->tune.chunk_spp;
+    out->compact = path_compact(s) ? 1 : 0;
+    out->_reserved = 0;
     return RT_OK;
 }
 

@@ -61,13 +61,18 @@ inline void sample_chunks(uint32_t W, uint32_t H, uint32_t spp, uint32_t& chunks
     chunks = (spp + chunk_spp - 1) / chunk_spp;
 }
 
+// PathWork::kinds value of a triangle-only scene whose triangle BVH runs in the
+// compact layout (rt_layout.h DevNodeC): kTris | 4, only with the 4-wave
+// resumable instance (api.cpp path_kinds).
+constexpr int kKindsCompact = 6;
+
 // Device workspace of one path-kernel launch (owned by the scene).
 struct PathWork {
     const DevScene* d_scene;  // the scene record in device memory (uploaded once)
     KParams* d_params;        // frame constants slot, staged by launch_path
     uint32_t waves;       // register budget of the kernel instance: 3 or 4 waves/SIMD
     bool resume;          // resumable triangle traversal (path_kernel RES)
-    int kinds;            // the scene's primitive kinds, kShapes 1 | kTris 2 (path_kernel KM)
+    int kinds;            // the scene's primitive kinds, kShapes 1 | kTris 2 (path_kernel KM); kKindsCompact
     uint32_t grid;        // persistent waves (path_grid)
     uint32_t* queue;      // wave-tile counter, zeroed by launch_path
     double* ring;         // [grid][kRing=8][64][3] finished-path radiance

@@ -190,18 +190,6 @@ RT_D bool shape_closest(const DevShape& s, V3 o, V3 d, const Rcp3& rc, bool rfas
     return false;
 }
 
-// Stack word of a pushed child (bvh_closest).  A leaf whose range fits is
-// packed as 1|count(7)|start(24), so resuming it loads nothing; an internal
-// child is its node index (count 0 is known); a leaf that does not fit is its
-// node index | kLeafRef, and its range is loaded on resume.  Node indices are
-// < 2^30 (checked by the host).
-constexpr uint32_t kPackedLeaf = 0x80000000u, kLeafRef = 0x40000000u;
-RT_D uint32_t child_word(uint32_t node, uint32_t start, uint32_t count) {
-    if (count == 0) return node;
-    if (count < 128u && start < (1u << 24)) return kPackedLeaf | (count << 24) | start;
-    return node | kLeafRef;
-}
-
 // BVH::intersection (bvh.rs:27-36) + Node::intersection (bvh.rs:151-186) as
 // a resumable per-lane state: the path kernel suspends a lane's triangle
 // traversal when few lanes of its wave are still traversing,
@@ -264,7 +252,34 @@ RT_D void trav_init(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
 // stepping through internal nodes; the wave tests leaf primitives once
 // >= kLeafBatch lanes wait (or every live lane does), so the primitive loop
 // runs with many lanes instead of a few.
-template <int KIND, int SLAB, bool ST, class Stk>
+// A child / stack word (child_word) -> the lane's current node: a packed leaf's
+// range, a big leaf's range from its node (f64 or compact layout), or an
+// internal node.
+template <bool CMP>
+RT_D void trav_enter(const DevBvh& B, Trav& T, uint32_t w) {
+    if (w & kPackedLeaf) { T.cnt = (w >> 24) & 127u; T.start = w & 0xFFFFFFu; }
+    else if (w & kLeafRef) {
+        T.node = w & ~kLeafRef;
+        if (CMP) { T.cnt = B.cnodes[T.node].count; T.start = B.cnodes[T.node].start; }
+        else { T.cnt = B.nodes[T.node].count; T.start = B.nodes[T.node].start; }
+    } else { T.node = w; T.cnt = 0; }
+}
+
+// A compact triangle record (rt_layout.h kTriC: a, b, c as f32) in registers:
+// ba = b - a and ca = c - a rebuilt in f64, the host's bits (triangle_props).
+struct F3 { float x, y, z; };
+RT_D TriRec load_tri_c(const float* __restrict__ p) {
+    const F3* q = (const F3*)p;
+    const F3 a = q[0], b = q[1], c = q[2];
+    asm volatile("" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(c.x), "v"(c.y), "v"(c.z));
+    const V3 A = v3(a.x, a.y, a.z);
+    return TriRec{A, v3(b.x, b.y, b.z) - A, v3(c.x, c.y, c.z) - A};
+}
+
+// CMP: the triangle BVH's compact layout (DevBvh::cnodes / ctris, KIND 3 only):
+// the same boxes and vertices as exact f32 copies, widened to f64 before the
+// same arithmetic — every lane's visits, tests and results are the f64 form's.
+template <int KIND, int SLAB, bool ST, bool CMP = false, class Stk>
 RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk& S, Cnt<ST>& C, Trav& T,
                     uint64_t lv, int leaf_batch = kLeafBatch) {
     const uint64_t at_leaf = __ballot(T.live && T.cnt != 0);
@@ -279,11 +294,11 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
                 // Software-pipelined leaf: the next triangle's record loads while this one
                 // is tested (C3 -0.8%, C5 -1.0% at reduced spp, variants_leafpipe_*.log).
                 const uint32_t end = T.start + T.cnt;
-                TriRec cur = load_tri(B.tris[T.start]);
+                TriRec cur = CMP ? load_tri_c(B.ctris + (size_t)T.start * kTriC) : load_tri(B.tris[T.start]);
                 for (uint32_t i = T.start; i < end; ++i) {
                     PH_COUNT(kPhLeafWave, kPhLeafLane);
                     TriRec nxt = cur;
-                    if (i + 1 < end) nxt = load_tri(B.tris[i + 1]);
+                    if (i + 1 < end) nxt = CMP ? load_tri_c(B.ctris + (size_t)(i + 1) * kTriC) : load_tri(B.tris[i + 1]);
                     double t, u = 0.0, v = 0.0;
                     C.tri();
                     const bool h = tri_uvt_r(cur, o, d, u, v, t);
@@ -307,7 +322,28 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
             }
             next = true;
         }
-    } else if (T.live && T.cnt == 0) {  // internal node (count 0 <=> children)
+    } else if (CMP && T.live && T.cnt == 0) {  // internal node, compact layout (one 64-B half line)
+        PH_COUNT(kPhInnerWave, kPhInnerLane);
+        const float4* nw = (const float4*)(B.cnodes + T.node);
+        const float4 w0 = nw[0], w1 = nw[1], w2 = nw[2];
+        const uint4 k = ((const uint4*)nw)[3];
+        asm volatile("" ::"v"(w1.z), "v"(w1.w), "v"(w2.x), "v"(w2.y), "v"(w2.z), "v"(w2.w));  // see node_boxes
+        double lt = 0.0, rt2 = 0.0;
+        C.aabb(2);
+        const bool lh = slab_v<SLAB>(v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), o, d, rc, fast, lt);
+        const bool rh = slab_v<SLAB>(v3(w1.z, w1.w, w2.x), v3(w2.y, w2.z, w2.w), o, d, rc, fast, rt2);
+        const double bt = T.best;  // +inf when no hit yet
+        const double li = lh ? (lt < bt ? lt : bt) : bt;
+        const double ri = rh ? (rt2 < bt ? rt2 : bt) : bt;
+        bool go_left = false;
+        if (li < bt) {
+            if (ri < bt) {
+                if (li < ri) { S.push(k.y, ri); go_left = true; }
+                else S.push(k.x, li);
+            } else go_left = true;
+        } else if (!(ri < bt)) next = true;
+        if (!next) trav_enter<true>(B, T, go_left ? k.x : k.y);
+    } else if (!CMP && T.live && T.cnt == 0) {  // internal node (count 0 <=> children)
         PH_COUNT(kPhInnerWave, kPhInnerLane);
         const DevNode& n = B.nodes[T.node];
         // the link words and the children's ranges, with the boxes (one 128-B line)
@@ -346,10 +382,7 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
             if (tt < T.best) { found = true; break; }
         }
         if (!found) T.live = false;
-        else if (w & kPackedLeaf) { T.cnt = (w >> 24) & 127u; T.start = w & 0xFFFFFFu; }
-        else if (w & kLeafRef) {
-            T.node = w & ~kLeafRef; T.cnt = B.nodes[T.node].count; T.start = B.nodes[T.node].start;
-        } else { T.node = w; T.cnt = 0; }
+        else trav_enter<CMP>(B, T, w);
     }
 }
 
@@ -1276,7 +1309,7 @@ RT_D uint32_t unit_of_row(const uint32_t* uq, uint32_t uq_back, uint32_t row) {
     return i % kUQ;
 }
 
-template <bool ST, bool HIT, int WAVES, bool RES, int KM = 3>
+template <bool ST, bool HIT, int WAVES, bool RES, int KM = 3, bool CMP = false>
 __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams Pv,
                                                      const DevScene* __restrict__ Sg,
                                                      const KParams* __restrict__ Pg, double* __restrict__ out,
@@ -1440,7 +1473,7 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
                     const bool can_take = next < min(win, open_end * kWave) || (!drained && next < win);
                     if (__ballot((busy && !q.T.live) || (!busy && can_take))) break;
                 }
-                trav_step<3, 2, ST>(S.tris, ps.o, ps.d, q.rc, q.fast, stk, C, q.T, lv, (int)P.leaf_batch);
+                trav_step<3, 2, ST, CMP>(S.tris, ps.o, ps.d, q.rc, q.fast, stk, C, q.T, lv, (int)P.leaf_batch);
             }
             PH_ADD(kPhTris, ph_t);
             // lanes whose query finished shade and end (or continue) their segment
@@ -1671,9 +1704,14 @@ PathFn path_fn_r(uint32_t waves, bool resume, int kinds) {
     return kinds == kShapes ? path_kernel<ST, HIT, 3, false, kShapes> : path_kernel<ST, HIT, 3, false>;
 #elif defined(RT_ONLY_C3)  // ... only the C3 instances
     (void)waves; (void)resume;
+    if (kinds == kKindsCompact) return path_kernel<ST, HIT, 4, true, kTris, true>;
     return kinds == kTris ? path_kernel<ST, HIT, 4, true, kTris> : path_kernel<ST, HIT, 4, true>;
 #else
-    if (waves == 4 && resume) return kinds == kTris ? path_kernel<ST, HIT, 4, true, kTris> : path_kernel<ST, HIT, 4, true>;
+    if (waves == 4 && resume) {
+        if (kinds == kKindsCompact) return path_kernel<ST, HIT, 4, true, kTris, true>;  // compact triangle layout
+        return kinds == kTris ? path_kernel<ST, HIT, 4, true, kTris> : path_kernel<ST, HIT, 4, true>;
+    }
+    kinds &= 3;  // the compact layout has only the triangle-only resumable instance (host: path_kinds)
     if (waves == 4) return path_kernel<ST, HIT, 4, false>;
     if (resume) return path_kernel<ST, HIT, 3, true>;
     return kinds == kShapes ? path_kernel<ST, HIT, 3, false, kShapes> : path_kernel<ST, HIT, 3, false>;

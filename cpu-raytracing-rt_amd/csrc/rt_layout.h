@@ -32,6 +32,36 @@ struct alignas(128) DevNode {
 };
 static_assert(sizeof(DevNode) == 128, "fat node is one 128-B line");
 
+// Stack / child word of a BVH child (render.hip trav_step): an internal child is
+// its node index (< 2^30, checked by the host); a leaf whose range fits is
+// packed as 1|count(7)|start(24), so reaching it loads nothing; a leaf that does
+// not fit is its node index | kLeafRef, and its range is loaded from the node.
+constexpr uint32_t kPackedLeaf = 0x80000000u, kLeafRef = 0x40000000u;
+#ifdef __HIPCC__
+__host__ __device__
+#endif
+inline uint32_t child_word(uint32_t node, uint32_t start, uint32_t count) {
+    if (count == 0) return node;
+    if (count < 128u && start < (1u << 24)) return kPackedLeaf | (count << 24) | start;
+    return node | kLeafRef;
+}
+
+// Compact triangle-BVH node (DESIGN.md §2 "compact layout"): both children's
+// boxes as f32 — exact copies, the host checks that every coordinate of the
+// f64 boxes round-trips through f32 — plus the children's words (child_word).
+// 64 B instead of 128: a visit reads four 16-B words.  A leaf's entry keeps its
+// own range (read through a kLeafRef word).  Same node numbering as DevNode.
+struct alignas(64) DevNodeC {
+    float lmin[3], lmax[3], rmin[3], rmax[3];
+    uint32_t lw, rw;            // child words of an internal node
+    uint32_t start, count;      // a leaf's own range
+};
+static_assert(sizeof(DevNodeC) == 64, "compact node is half a line");
+// Compact triangle record: the vertices a, b, c as f32 (36 B, exact copies; the
+// device rebuilds ba = b - a, ca = c - a in f64 — the same bits as the host's,
+// which triangle_props computed from the same a, b, c).
+constexpr uint32_t kTriC = 9;   // floats per compact triangle record
+
 struct alignas(16) DevShape {  // Primitive<T> hot part (scene.rs:20-27)
     double shape[3];           // plane normal | box half sizes | ellipsoid radii
     double pos[3];
@@ -87,6 +117,10 @@ struct DevBvh {
     const double* tri_inv_area;
     const uint32_t* mat;       // material per primitive
     const int32_t* gid;        // global primitive id per primitive
+    // the compact layout of a triangle BVH (DevNodeC + kTriC floats per triangle),
+    // non-null only when every box coordinate and vertex is an exact f32
+    const DevNodeC* cnodes;
+    const float* ctris;
 };
 
 struct DevScene {

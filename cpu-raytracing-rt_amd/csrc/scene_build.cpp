@@ -290,7 +290,7 @@ static uint32_t shape_flags(const rt_shape& s, uint32_t& axis) {
 }
 
 struct ShapeItem { DevShape s; uint32_t mat; int32_t gid; Box3 box; };
-struct TriItem { Triangle t; uint32_t mat; int32_t gid; Box3 box; };
+struct TriItem { Triangle t; V3 b, c; uint32_t mat; int32_t gid; Box3 box; };  // b, c: the vertices t was built from
 
 void build_shape_bvh(const std::vector<ShapeItem>& items, HostBvhArrays& out) {
     std::vector<Box3> boxes(items.size());
@@ -304,11 +304,53 @@ void build_shape_bvh(const std::vector<ShapeItem>& items, HostBvhArrays& out) {
         out.gid.push_back(items[i].gid);
     }
 }
-void build_tri_bvh(const std::vector<TriItem>& items, HostBvhArrays& out) {
+bool f32_exact(double v) { return (double)(float)v == v || v != v; }
+bool f32_exact3(V3 v) { return f32_exact(v.x) && f32_exact(v.y) && f32_exact(v.z) && v.x == v.x && v.y == v.y && v.z == v.z; }
+
+// The compact layout (rt_layout.h DevNodeC + kTriC floats): built only when it
+// holds the same numbers — every child-box coordinate and every vertex a, b, c
+// is an exact f32 (glTF positions are f32: C3-C5; a custom TRIANGLE rotated by a
+// quaternion usually is not).  The device widens them back to f64 and rebuilds
+// ba = b - a, ca = c - a: the bits triangle_props computed from the same a, b, c.
+void build_compact(const HostBvh& h, const std::vector<TriItem>& items, HostBvhArrays& out) {
+    for (const HostNode& n : h.nodes)
+        if (!f32_exact3(n.box.min) || !f32_exact3(n.box.max)) return;
+    for (const TriItem& it : items)
+        if (!f32_exact3(it.t.a) || !f32_exact3(it.b) || !f32_exact3(it.c)) return;
+    std::vector<DevNodeC> cn(h.nodes.size());
+    auto put3 = [](float* d, V3 v) { d[0] = (float)v.x; d[1] = (float)v.y; d[2] = (float)v.z; };
+    for (size_t i = 0; i < h.nodes.size(); ++i) {
+        const HostNode& n = h.nodes[i];
+        DevNodeC c;
+        std::memset(&c, 0, sizeof(c));
+        if (n.left >= 0) {
+            const HostNode& l = h.nodes[n.left];
+            const HostNode& r = h.nodes[n.right];
+            if ((uint64_t)n.left != i + 1) return;  // pre-order: the left child follows its parent
+            put3(c.lmin, l.box.min); put3(c.lmax, l.box.max);
+            put3(c.rmin, r.box.min); put3(c.rmax, r.box.max);
+            c.lw = child_word((uint32_t)n.left, (uint32_t)l.start, (uint32_t)(l.end - l.start));
+            c.rw = child_word((uint32_t)n.right, (uint32_t)r.start, (uint32_t)(r.end - r.start));
+        }
+        c.start = (uint32_t)n.start;
+        c.count = (uint32_t)(n.end - n.start);
+        cn[i] = c;
+    }
+    std::vector<float> ct(items.size() * kTriC);
+    for (size_t k = 0; k < h.order.size(); ++k) {
+        const TriItem& it = items[h.order[k]];
+        put3(&ct[k * kTriC], it.t.a); put3(&ct[k * kTriC + 3], it.b); put3(&ct[k * kTriC + 6], it.c);
+    }
+    out.cnodes = std::move(cn);
+    out.ctris = std::move(ct);
+}
+
+void build_tri_bvh(const std::vector<TriItem>& items, HostBvhArrays& out, bool compact = false) {
     std::vector<Box3> boxes(items.size());
     for (size_t i = 0; i < items.size(); ++i) boxes[i] = items[i].box;
     HostBvh h = build_bvh(boxes);
     flatten(h, out);
+    if (compact && !h.nodes.empty()) build_compact(h, items, out);
     out.n_prims = (uint32_t)items.size();
     out.tris.reserve(items.size());
     for (uint64_t i : h.order) {
@@ -440,6 +482,8 @@ std::string build_scene(const rt_scene_desc& d, HostScene& out) {
         if (d.tri_mode == RT_TRI_GLTF) {  // new_with_smooth_normal + instantiate (gltf/scene_builder.rs:42-55)
             const double* nn = d.tri_normals + 9 * j;
             it.t = triangle_smooth(load3(v), load3(v + 3), load3(v + 6), load3(nn), load3(nn + 3), load3(nn + 6));
+            it.b = load3(v + 3);
+            it.c = load3(v + 6);
             Box3 b = box_empty();
             box_extend(b, it.t.a);
             box_extend(b, it.t.a + it.t.ba);
@@ -453,6 +497,8 @@ std::string build_scene(const rt_scene_desc& d, HostScene& out) {
             V3 b = rotate(rot, m.ba + m.a) + pos;
             V3 c = rotate(rot, m.ca + m.a) + pos;
             it.t = triangle_smooth(a, b, c, rotate(rot, m.na), rotate(rot, m.nb), rotate(rot, m.nc));
+            it.b = b;
+            it.c = c;
             Box3 bb = box_empty();
             box_extend(bb, a); box_extend(bb, b); box_extend(bb, c);
             it.box = bb;
@@ -466,7 +512,7 @@ std::string build_scene(const rt_scene_desc& d, HostScene& out) {
     for (auto& it : tris) if (is_light(d.materials[it.mat])) ltris.push_back(it);
     build_shape_bvh(boxes, out.bvh[0]);
     build_shape_bvh(ells, out.bvh[1]);
-    build_tri_bvh(tris, out.bvh[2]);
+    build_tri_bvh(tris, out.bvh[2], true);  // the scene's triangle BVH: compact layout when exact
     build_shape_bvh(lboxes, out.bvh[3]);
     build_shape_bvh(lells, out.bvh[4]);
     build_tri_bvh(ltris, out.bvh[5]);

@@ -49,6 +49,10 @@ struct HostBvhArrays {
     std::vector<double> tri_inv_area;
     std::vector<uint32_t> mat;
     std::vector<int32_t> gid;
+    // compact layout of a triangle BVH (rt_layout.h DevNodeC, kTriC floats per
+    // triangle): filled only when every box coordinate and vertex is an exact f32
+    std::vector<DevNodeC> cnodes;
+    std::vector<float> ctris;
 };
 struct HostScene {
     std::vector<DevMaterial> mats;

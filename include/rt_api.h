@@ -182,8 +182,12 @@ typedef struct rt_scene_info {
        pdf of a diffuse bounce comes from the next segment's box tests (DESIGN.md
        §4 "shared light tests"); 0 = separate light queries */
     uint32_t shared_light_mask;
-    uint32_t reserved;
+    /* RT_LAYOUT_COMPACT_TRIS: the triangle BVH also has its compact layout (f32
+       child boxes and vertices, every one an exact copy of the f64 value; DESIGN.md
+       §2), which the resumable triangle-only kernel reads */
+    uint32_t layout_flags;
 } rt_scene_info;
+#define RT_LAYOUT_COMPACT_TRIS 0x1u
 int rt_scene_get_info(const rt_scene* scene, rt_scene_info* out);
 
 /* Kernel form of a scene's renders.  The library picks every
@@ -199,6 +203,9 @@ typedef struct rt_tuning {
     uint32_t suspend_lanes;  /* 0 auto (24 cache-resident BVH, 40 HBM-streamed); 1..64                   */
     uint32_t leaf_lanes;     /* 0 auto (32 cache-resident BVH, 24 HBM-streamed); 1..64                   */
     uint32_t chunk_spp;      /* 0 the frame's rule (rt_sample_chunks); else the sample run length        */
+    int32_t  compact;        /* -1 auto (1 when the scene has it: RT_LAYOUT_COMPACT_TRIS); 0 the f64
+                                triangle-BVH layout; 1 the compact one (triangle-only resumable kernel) */
+    uint32_t _reserved;
 } rt_tuning;
 /* NULL restores every field to auto.  Fields out of range -> RT_ERR_INVALID. */
 int rt_scene_set_tuning(rt_scene* scene, const rt_tuning* tuning);

@@ -43,10 +43,13 @@ def hairball(rt, orc, tmp_path_factory):
     return desc, params, rt.Scene(desc), orc.OracleScene(desc)
 
 
-def test_hairball(hairball):
+def test_hairball(hairball, segment_form):
     desc, params, g, o = hairball
     img, _, st = _compare(g, o, params)
     assert st["tri_tests"] > 0 and st["shaded_hits"] > 0
+    # glTF positions are f32: the compact triangle layout exists and the resumable forms read it
+    assert g.info()["layout_flags"] == 1
+    assert g.tuning()["compact"] == (1 if segment_form in ("resume", "resume_eager") else 0)
 
 
 def test_room(room):

@@ -34,7 +34,7 @@ def sink(rt, orc, scene_text):
 FORM = {}
 
 
-@pytest.fixture(autouse=True, params=["fused", "resume", "resume_eager", "general"])
+@pytest.fixture(autouse=True, params=["fused", "resume", "resume_eager", "resume_f64", "general"])
 def segment_form(request):
     """Every test runs both path-kernel segment forms: fused (whole closest-hit
     query, then shading) and resumable (triangle traversal suspended while few
@@ -43,11 +43,16 @@ def segment_form(request):
     (suspend_lanes=64, leaf_lanes=1: the far ends of the per-scene knobs the
     host picks, api.cpp path_suspend / path_leaf_batch).
     "general" is the fused form in its all-kinds instance (kinds=3) where the
-    host would pick a shape-only or triangle-only one (api.cpp path_kinds)."""
+    host would pick a shape-only or triangle-only one (api.cpp path_kinds).
+    The resumable forms read a glTF scene's triangle BVH in its compact layout
+    (f32 child boxes and vertices, exact copies: api.cpp path_compact);
+    "resume_f64" forces the f64 layout in the same kernel."""
     FORM.clear()
     FORM["resume"] = 1 if request.param.startswith("resume") else 0
     if request.param == "resume_eager":
         FORM.update(suspend_lanes=64, leaf_lanes=1)
+    if request.param == "resume_f64":
+        FORM["compact"] = 0
     if request.param == "general":
         FORM["kinds"] = 3
     yield request.param
@@ -455,6 +460,21 @@ def test_deep_stack_and_big_leaf(rt, orc):
     pd = rays.copy()
     pd[:, 3:] /= np.linalg.norm(pd[:, 3:], axis=1, keepdims=True)
     assert np.array_equal(g.light_pdf(pd), o.light_pdf(pd))
+
+
+def test_deep_stack_and_big_leaf_render(rt, orc):
+    """The same 21-level chain with f32-exact coordinates, so the triangle BVH also has
+    its compact layout (rt_layout.h DevNodeC): whole paths through the LDS + spill
+    stack and the 149-triangle leaf (a kLeafRef child word) in every kernel form,
+    the 4-wave instance forced so the resumable forms read the compact layout."""
+    desc = _deep_chain(rt)
+    desc.tri_vertices = desc.tri_vertices.astype(np.float32).astype(np.float64)
+    g, o = rt.Scene(desc), orc.OracleScene(desc)
+    info = g.info()
+    assert info["layout_flags"] == 1 and info["bvh_depth"][2] > 12 + 6
+    p = rt.RenderParams(width=24, height=16, spp=2, ray_depth=4, cam_position=(0.0, 0.0, -1.0), fov=0.6)
+    img, _, st = _compare(g, o, p, waves=4)
+    assert st["tri_tests"] > 0 and st["shaded_hits"] > 0
 
 
 def _tri_boxes(desc):
