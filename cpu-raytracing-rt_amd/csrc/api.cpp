@@ -696,7 +696,8 @@ int rt_intersect_rays_async(rt_scene* s, const double* d_rays, uint32_t n, rt_hi
     if (rc) return rc;
     if (!s->queue) HIP_TRY(hipMalloc(&s->queue, kQueueWords * sizeof(uint32_t)));
     HIP_TRY(ws_begin(s, st));
-    HIP_TRY(launch_trace(s->dev, d_rays, n, d_out, s->queue, s->spill_n, s->spill_t, grid, st));
+    // the persistent form reads the compact triangle layout when the scene has it (rt_tuning.compact)
+    HIP_TRY(launch_trace(s->dev, d_rays, n, d_out, s->queue, s->spill_n, s->spill_t, grid, s->tune.compact != 0, st));
     HIP_TRY(ws_end(s, st));
     return RT_OK;
 }

@@ -105,7 +105,7 @@ hipError_t launch_path(const DevScene& S, const KParams& P, const PathWork& W, d
                        unsigned long long* stats, hipStream_t st);
 hipError_t launch_reduce_chunks(const double* part, double* out, const KParams& P, hipStream_t st);
 hipError_t launch_trace(const DevScene& S, const double* rays, uint32_t n, rt_hit* out, uint32_t* queue,
-                        uint32_t* spill_n, double* spill_t, uint32_t grid, hipStream_t st);
+                        uint32_t* spill_n, double* spill_t, uint32_t grid, bool compact, hipStream_t st);
 hipError_t trace_grid(uint32_t n, uint32_t* grid);
 hipError_t launch_intersect(const DevScene& S, const double* rays, uint32_t n, rt_hit* out, uint32_t* spill_n,
                             double* spill_t, hipStream_t st);

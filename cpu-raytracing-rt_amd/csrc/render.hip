@@ -276,6 +276,11 @@ RT_D TriRec load_tri_c(const float* __restrict__ p) {
     return TriRec{A, v3(b.x, b.y, b.z) - A, v3(c.x, c.y, c.z) - A};
 }
 
+#ifdef RT_RECOMPUTE_UV  // experiment: the compact kernel re-tests the winner for (u, v) instead of carrying them
+constexpr bool kRecomputeUV = true;
+#else
+constexpr bool kRecomputeUV = false;
+#endif
 // CMP: the triangle BVH's compact layout (DevBvh::cnodes / ctris, KIND 3 only):
 // the same boxes and vertices as exact f32 copies, widened to f64 before the
 // same arithmetic — every lane's visits, tests and results are the f64 form's.
@@ -303,7 +308,8 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
                     C.tri();
                     const bool h = tri_uvt_r(cur, o, d, u, v, t);
                     if (h && (!T.valid || t < T.best)) {  // update_best_intersection (bvh.rs:213-222)
-                        T.valid = true; T.best = t; T.bu = u; T.bv = v; T.prim = i; T.aux = 0;
+                        T.valid = true; T.best = t; T.prim = i; T.aux = 0;
+                        if (!(CMP && kRecomputeUV)) { T.bu = u; T.bv = v; }
                     }
                     cur = nxt;
                 }
@@ -1168,13 +1174,17 @@ RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, P
 }
 
 // the resumable form's end of a segment: finish `intersect`, then shade
-template <bool ST, int KM = 3, class Stk>
+template <bool ST, int KM = 3, bool CMP = false, class Stk>
 RT_D bool segment_end(const DevScene& S, const KParams& P, const Scales& sc, PathState& ps, Rng& rng,
                       Stk& stk, Cnt<ST>& C, SegQuery& q, int32_t& hit_gid, bool last) {
     Hit h; uint32_t mat = 0; int32_t gid = 0;
     if (KM == kTris) {  // the candidate is the triangle traversal's (take_tri on an empty best)
         q.best.valid = false; q.best.t = 0.0; q.best.u = q.best.v = 0.0; q.best.prim = 0; q.best.aux = 0;
         q.best.kind = 0;
+    }
+    if (CMP && kRecomputeUV && q.T.valid) {  // the winner's (u, v): the same test, the same bits
+        double t;
+        (void)tri_uvt_r(load_tri_c(S.tris.ctris + (size_t)q.T.prim * kTriC), ps.o, ps.d, q.T.bu, q.T.bv, t);
     }
     take_tri(q.best, q.T.valid, q.T.best, q.T.bu, q.T.bv, q.T.prim);
     const bool hit = intersect_tail<ST, KM>(S, q.best, ps.o, ps.d, C, h, mat, gid);
@@ -1323,6 +1333,9 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
     // camera rays of the next kCamSlots paths, [component][slot] (fused kernel only)
     __shared__ double s_cam[RES ? 1 : 3 * kCamSlots];
     __shared__ uint32_t s_uq[kUQ * kUW];  // open wave-tiles (store_unit)
+#ifdef RT_SUM_LDS  // experiment: the lane's committed-row sum in LDS instead of 6 VGPRs
+    __shared__ double s_sum[3 * kWave];
+#endif
     const uint32_t lane = threadIdx.x;
     auto stk = make_stack<RES>(s_n, s_t, 0u, (uint64_t)blockIdx.x * kWave, spill_n, spill_t,
                            gridDim.x * kWave);
@@ -1346,7 +1359,11 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
     const unsigned long long ph_tile = PH_T();
     if (lane < kRing) s_cnt[lane] = 0;
     __syncthreads();
+#ifdef RT_SUM_LDS
+    s_sum[lane] = 0.0; s_sum[kWave + lane] = 0.0; s_sum[2 * kWave + lane] = 0.0;
+#else
     V3 sum = v3(0.0, 0.0, 0.0);
+#endif
     uint32_t base = 0, next = 0, witers = 0;  // wave-uniform: next row to commit, next path to hand out
     uint32_t open_end = 0;                    // rows of the wave-tiles pulled so far
     uint32_t uq_front = 0, uq_back = 0;       // open wave-tiles: s_uq entries [uq_front, uq_back)
@@ -1483,7 +1500,7 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
                 if (inq) {
                     int32_t g;
                     const unsigned long long ph_s = PH_T();
-                    cont = segment_end<ST, KM>(S, P, sc, ps, rng, stk, C, q, g, b + 1 >= depth);
+                    cont = segment_end<ST, KM, CMP>(S, P, sc, ps, rng, stk, C, q, g, b + 1 >= depth);
                     PH_ADDW(kPhSegment, ph_s);
                     if (HIT) hit_ids[(pixel * P.spp + s) * depth + b] = g;
                     ++b;
@@ -1519,7 +1536,12 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
         __syncthreads();
         while (base < open_end && s_cnt[base % kRing] == (uint32_t)kWave) {
             const double* rp = ring + ((uint64_t)(base % kRing) * kWave + lane) * 3;
+#ifdef RT_SUM_LDS
+            V3 sum = v3(s_sum[lane], s_sum[kWave + lane], s_sum[2 * kWave + lane]) + v3(rp[0], rp[1], rp[2]);
+            s_sum[lane] = sum.x; s_sum[kWave + lane] = sum.y; s_sum[2 * kWave + lane] = sum.z;
+#else
             sum = sum + v3(rp[0], rp[1], rp[2]);
+#endif
             __syncthreads();
             if (lane == 0) s_cnt[base % kRing] = 0;
             __syncthreads();
@@ -1532,7 +1554,11 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
                 const V3 res = own ? (Pt.chunks == 1 ? sum / (double)Pt.spp : sum) : v3(0.0, 0.0, 0.0);
                 double* o = (Pt.chunks == 1 ? out : part) + ((uint64_t)e[4] * kBlock + ly * RT_TILE + lx) * 3;
                 o[0] = res.x; o[1] = res.y; o[2] = res.z;
+#ifdef RT_SUM_LDS
+                s_sum[lane] = 0.0; s_sum[kWave + lane] = 0.0; s_sum[2 * kWave + lane] = 0.0;
+#else
                 sum = v3(0.0, 0.0, 0.0);
+#endif
                 ++uq_front;
             }
             ++base;
@@ -1566,7 +1592,7 @@ RT_D void write_hit(rt_hit* __restrict__ out, uint32_t i, bool ok, const Hit& h,
     out[i] = r;
 }
 
-template <int WAVES>
+template <int WAVES, bool CMP = false>  // CMP: the triangle BVH's compact layout (trav_step)
 __global__ __launch_bounds__(kWave, WAVES) void trace_kernel(DevScene S, const double* __restrict__ rays,
                                                              uint32_t n, rt_hit* __restrict__ out,
                                                              uint32_t* __restrict__ queue, uint32_t* spill_n,
@@ -1601,7 +1627,7 @@ __global__ __launch_bounds__(kWave, WAVES) void trace_kernel(DevScene S, const d
             }
         }
         const uint64_t lv2 = __ballot(q.T.live);
-        if (lv2) trav_step<3, 2, false>(S.tris, ps.o, ps.d, q.rc, q.fast, stk, C, q.T, lv2);
+        if (lv2) trav_step<3, 2, false, CMP>(S.tris, ps.o, ps.d, q.rc, q.fast, stk, C, q.T, lv2);
         if (has && !q.T.live) {
             Hit h; uint32_t mat = 0; int32_t gid = 0;
             take_tri(q.best, q.T.valid, q.T.best, q.T.bu, q.T.bv, q.T.prim);
@@ -1785,10 +1811,14 @@ hipError_t launch_intersect(const DevScene& S, const double* rays, uint32_t n, r
 }
 // persistent batch intersect (trace_kernel): grid = resident waves, capped by the rays
 hipError_t launch_trace(const DevScene& S, const double* rays, uint32_t n, rt_hit* out, uint32_t* queue,
-                        uint32_t* spill_n, double* spill_t, uint32_t grid, hipStream_t st) {
+                        uint32_t* spill_n, double* spill_t, uint32_t grid, bool compact, hipStream_t st) {
     hipError_t e = hipMemsetAsync(queue, 0, kQueueWords * sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(trace_kernel<4>, dim3(grid), dim3(kWave), 0, st, S, rays, n, out, queue, spill_n, spill_t);
+    if (compact && S.tris.cnodes)
+        hipLaunchKernelGGL((trace_kernel<4, true>), dim3(grid), dim3(kWave), 0, st, S, rays, n, out, queue, spill_n,
+                           spill_t);
+    else
+        hipLaunchKernelGGL(trace_kernel<4>, dim3(grid), dim3(kWave), 0, st, S, rays, n, out, queue, spill_n, spill_t);
     return hipGetLastError();
 }
 hipError_t trace_grid(uint32_t n, uint32_t* grid) {

@@ -315,7 +315,8 @@ int rt_intersect_rays(rt_scene* scene, const double* rays, uint32_t n, rt_hit* o
 /* The same query on device-resident buffers, stream-ordered (no host copies):
    d_rays [n][6] f64 and d_out [n] rt_hit in HBM.  method 0 runs one thread per
    ray; method 1 the persistent traversal (waves refill finished lanes from a
-   queue).  Both give identical hits.  Uses the scene's workspace, ordered
+   queue), on the triangle BVH's compact layout when the scene has it and its
+   tuning allows (rt_tuning.compact).  Both give identical hits.  Uses the scene's workspace, ordered
    after the scene's previous launch (Conventions: Streams). */
 #define RT_TRACE_PER_RAY    0
 #define RT_TRACE_PERSISTENT 1

@@ -84,10 +84,12 @@ def test_atrium_intersect_random(atrium):
     assert (gh["prim"] >= 0).mean() > 0.75   # open-roofed atrium: upward rays may escape
 
 
-@pytest.mark.parametrize("method", [0, 1])
-def test_atrium_intersect_device(atrium, rt, method):
-    """Deep triangle BVH through both device batch kernels: the oracle's hits."""
+@pytest.mark.parametrize("method,compact", [(0, -1), (1, -1), (1, 0)])
+def test_atrium_intersect_device(atrium, rt, method, compact):
+    """Deep triangle BVH through both device batch kernels (the persistent one on the
+    compact triangle layout, and forced to the f64 one): the oracle's hits."""
     desc, params, g, o = atrium
+    g.set_tuning(compact=compact)
     rng = np.random.default_rng(14)
     n = 30000
     pos = np.stack([rng.uniform(-10, 10, n), rng.uniform(0.5, 11, n), rng.uniform(-5, 5, n)], axis=1)

@@ -94,7 +94,20 @@ for s in $STEPS; do
              -- $B --workload C5 --steps 2 --warmup 1 --no-cpu-baseline --no-pmc || exit 1 ;;
     var5)  run variants_C5 900 python3 tools/variants.py C5 ${VAR_SPP5:-16} \
              ${VARIANTS:-cpu-raytracing-rt_amd/build*/librt_amd.so} || exit 1 ;;
-    *) echo "unknown step $s"; exit 2 ;;
+    calib)  # FETCH_SIZE / TCC_EA0_RDREQ* factors for the traversal's record gathers (tools/fetch_calib.hip)
+      run calib_plain 120 tools/fetch_calib || exit 1
+      run calib_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/calib_fetch" -o run \
+        -- tools/fetch_calib || exit 1
+      run calib_rdreq 120 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum \
+        TCC_EA0_RDREQ_128B_sum --output-format csv -d "$OUT/calib_rdreq" -o run -- tools/fetch_calib || exit 1
+      run calib_dram 120 rocprofv3 --pmc TCC_EA0_RDREQ_DRAM_sum TCC_HIT_sum TCC_MISS_sum --output-format csv \
+        -d "$OUT/calib_dram" -o run -- tools/fetch_calib || exit 1
+      run calib_report 60 python3 tools/fetch_calib.py "$OUT" || exit 1 ;;
+    pcs2|pcs3|pcs5)  # host-trap PC sampling of the path kernel (where its wave-time goes, per instruction)
+      w=C${s#pcs}
+      run pcs_$w 420 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method host_trap --pc-sampling-unit time \
+        --pc-sampling-interval ${PCS_INTERVAL:-1} --output-format csv -d "$OUT/pcs_$w" -o run \
+        -- $B --workload $w --spp ${PCS_SPP:-16} --steps 1 --warmup 0 --no-cpu-baseline --no-pmc || exit 1 ;;
   esac
 done
 echo "[$(date +%T)] batch done"
