@@ -472,9 +472,33 @@ def test_deep_stack_and_big_leaf_render(rt, orc):
     g, o = rt.Scene(desc), orc.OracleScene(desc)
     info = g.info()
     assert info["layout_flags"] == 1 and info["bvh_depth"][2] > 12 + 6
-    p = rt.RenderParams(width=24, height=16, spp=2, ray_depth=4, cam_position=(0.0, 0.0, -1.0), fov=0.6)
+    f = np.array([0.0, -0.4, 1.0]) / np.sqrt(1.16)
+    u = np.array([0.0, 1.0, 0.4]) / np.sqrt(1.16)
+    p = rt.RenderParams(width=24, height=16, spp=2, ray_depth=4, cam_position=(0.0, 0.5, -1.0),
+                        cam_forward=tuple(f), cam_up=tuple(u), fov=0.9)
     img, _, st = _compare(g, o, p, waves=4)
     assert st["tri_tests"] > 0 and st["shaded_hits"] > 0
+
+
+def test_deep_stack_and_big_leaf_compact_trace(rt, orc):
+    """The persistent batch trace kernel on the compact layout (rt_intersect_rays_async
+    method 1): in-plane rays along the f32-exact chain push past the LDS stack into the
+    spill area and reach the 149-triangle leaf through its kLeafRef child word."""
+    desc = _deep_chain(rt)
+    desc.tri_vertices = desc.tri_vertices.astype(np.float32).astype(np.float64)
+    g, o = rt.Scene(desc), orc.OracleScene(desc)
+    rng = np.random.default_rng(12)
+    n = 4096
+    orig = np.stack([rng.uniform(-0.9, 0.9, n), np.zeros(n), np.full(n, -1.0)], axis=1)
+    d = np.stack([rng.uniform(-1e-6, 1e-6, n), np.zeros(n), np.ones(n)], axis=1)
+    d[: n // 2, 0] = 0.0
+    rays = np.concatenate([orig, d], axis=1)
+    oh = o.intersect(rays)
+    for compact in (-1, 0):
+        g.set_tuning(compact=compact)
+        gh = intersect_device(rt, g, rays, 1)
+        assert np.array_equal(gh.view(np.uint8), oh.view(np.uint8)), compact
+    assert (oh["prim"][: n // 2] == len(desc.tri_material) - 1).all()
 
 
 def _tri_boxes(desc):
