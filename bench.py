@@ -158,16 +158,26 @@ def pmc_counters(args, world):
 
 
 def hbm_traffic(pmc):
-    """HBM bytes per launch.  Correction per MI355X_MICROARCH.md "HBM": FETCH_SIZE
-    is in KiB and reports half the bytes of 16-B/lane loads on gfx950 (the
-    node/triangle loads are dwordx4), so fetch = 2 * 1024 * FETCH_SIZE;
-    WRITE_SIZE is taken as reported (KiB)."""
+    """Memory-side bytes per launch.  Correction per MI355X_MICROARCH.md "HBM":
+    FETCH_SIZE is in KiB and reports half the bytes on gfx950, so fetch = 2 *
+    1024 * FETCH_SIZE; WRITE_SIZE is taken as reported (KiB).  The x2 factor is
+    calibrated for the traversal's own access pattern (tools/fetch_calib.hip,
+    profiles/r03/fetch_calib.log): for dependent random gathers of 128-B fat
+    nodes, 80-B / 36-B triangle records and 64-B compact nodes, over a 128-MiB
+    (Infinity-Cache-resident) and a 4-GiB table, 2 x 1024 x FETCH_SIZE equals
+    the 128-B-line bytes the L2 requested from the memory side (TCC_EA0_RDREQ
+    by size) within 3%, MALL hits included (TCC_EA0_RDREQ_DRAM counts them
+    too).  So `fetch` is line bytes past the L2, MALL + DRAM; it is >= the
+    algorithmic bytes (1.0x for 128-B records, 2.0x for 64-B, 2.4x for 80-B,
+    4.4x for 36-B)."""
     fetch = 2.0 * 1024.0 * pmc["FETCH_SIZE"]
     write = 1024.0 * pmc["WRITE_SIZE"]
     return fetch + write, {"FETCH_SIZE_KiB": pmc["FETCH_SIZE"], "WRITE_SIZE_KiB": pmc["WRITE_SIZE"],
                            "fetch_bytes": fetch, "write_bytes": write,
-                           "correction": "fetch = 2 x 1024 x FETCH_SIZE (gfx950 16-B/lane loads); "
-                                         "write = 1024 x WRITE_SIZE", "kernel": PATH_KERNEL}
+                           "correction": "fetch = 2 x 1024 x FETCH_SIZE = 128-B-line bytes past the L2 (MALL + "
+                                         "DRAM), calibrated for the traversal's gathers in "
+                                         "profiles/r03/fetch_calib.log; write = 1024 x WRITE_SIZE",
+                           "kernel": PATH_KERNEL}
 
 
 def valu_roofline(pmc, pmc_ns, kern_s):

@@ -14,6 +14,8 @@ for group in ("calib_fetch", "calib_rdreq", "calib_dram"):
         for f in files:
             if f.endswith("counter_collection.csv"):
                 for row in csv.DictReader(open(os.path.join(root, f))):
+                    if "gather<" not in row["Kernel_Name"]:
+                        continue  # the table fills (hipMemset) are dispatches too
                     d = int(row["Dispatch_Id"])
                     counters.setdefault(d, {})
                     counters[d][row["Counter_Name"]] = counters[d].get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
