@@ -237,8 +237,8 @@ int ensure_part(rt_scene* s, const KParams& k) {
 // deepest BVH, one slot per launched lane.
 int ensure_spill(rt_scene* s, uint64_t lanes) {
     uint32_t depth = s->dev.max_depth;
-    if (depth <= (uint32_t)kMaxBvhDepthShort) return RT_OK;
-    size_t need = (size_t)(depth - kMaxBvhDepthShort) * lanes;
+    if (depth <= (uint32_t)kMinShort) return RT_OK;
+    size_t need = (size_t)(depth - kMinShort) * lanes;
     if (need <= s->spill_entries) return RT_OK;
     if (int rc = ws_idle(s)) return rc;
     if (s->spill_n) (void)hipFree(s->spill_n);

@@ -51,7 +51,7 @@ RT_D uint32_t stack_lane() {
 }
 // OPQ = false keeps the lane index in a register (the 3-wave fused kernel,
 // which has room: C2 113.8 vs 115.1 ms with OPQ); OPQ = true recomputes it.
-template <bool OPQ>
+template <bool OPQ, int KS = kShort>  // KS: LDS entries per lane
 struct Stack {
     uint32_t* sn;        // LDS node slots of this wave, [slot][lane]
     double* st;          // LDS entry-t slots of this wave, [slot][lane]
@@ -63,8 +63,8 @@ struct Stack {
     RT_D uint32_t lane() const { return OPQ ? stack_lane() : ln; }
     RT_D void push(uint32_t node, double t) {
         const uint32_t l = lane();
-        if (sp < kShort) { sn[sp * kWave + l] = node; st[sp * kWave + l] = t; }
-        else { gn[(size_t)(sp - kShort) * stride + l] = node; gt[(size_t)(sp - kShort) * stride + l] = t; }
+        if (sp < KS) { sn[sp * kWave + l] = node; st[sp * kWave + l] = t; }
+        else { gn[(size_t)(sp - KS) * stride + l] = node; gt[(size_t)(sp - KS) * stride + l] = t; }
         ++sp;
     }
     // The spill side reads through volatile pointers: otherwise the compiler
@@ -73,21 +73,21 @@ struct Stack {
     RT_D void pop(uint32_t& node, double& t) {
         --sp;
         const uint32_t l = lane();
-        if (sp < kShort) { node = sn[sp * kWave + l]; t = st[sp * kWave + l]; }
+        if (sp < KS) { node = sn[sp * kWave + l]; t = st[sp * kWave + l]; }
         else {
-            node = ((volatile const uint32_t*)gn)[(size_t)(sp - kShort) * stride + l];
-            t = ((volatile const double*)gt)[(size_t)(sp - kShort) * stride + l];
+            node = ((volatile const uint32_t*)gn)[(size_t)(sp - KS) * stride + l];
+            t = ((volatile const double*)gt)[(size_t)(sp - KS) * stride + l];
         }
     }
 };
 // wave_tid = the wave's first thread in the block, wave_gtid = its first
 // thread in the grid (both wave-uniform)
-template <bool OPQ = false>
-RT_D Stack<OPQ> make_stack(uint32_t* s_n, double* s_t, uint32_t wave_tid, uint64_t wave_gtid, uint32_t* spill_n,
-                           double* spill_t, uint32_t spill_stride) {
-    Stack<OPQ> k;
+template <bool OPQ = false, int KS = kShort>
+RT_D Stack<OPQ, KS> make_stack(uint32_t* s_n, double* s_t, uint32_t wave_tid, uint64_t wave_gtid, uint32_t* spill_n,
+                               double* spill_t, uint32_t spill_stride) {
+    Stack<OPQ, KS> k;
     k.ln = __lane_id();
-    const uint32_t base = (wave_tid / kWave) * kShort * kWave;
+    const uint32_t base = (wave_tid / kWave) * KS * kWave;
     k.sn = s_n + base; k.st = s_t + base;
     k.gn = spill_n ? spill_n + wave_gtid : nullptr;
     k.gt = spill_t ? spill_t + wave_gtid : nullptr;
@@ -1319,16 +1319,48 @@ RT_D uint32_t unit_of_row(const uint32_t* uq, uint32_t uq_back, uint32_t row) {
     return i % kUQ;
 }
 
+// waves per SIMD the 4-wave resumable kernel's register budget must allow (experiment: 5)
+#ifndef RT_RES_OCC
+#define RT_RES_OCC 4
+#endif
+constexpr int kResOcc = RT_RES_OCC;
+
+// A lane's throughput T and radiance L in the wave's LDS block, [component][lane]
+// (the 4-wave resumable kernel).  The lane index is re-derived (stack_lane), so
+// it is not held in a register across the traversal either.
+#ifdef RT_NO_LDS_TL  // ablation build: T and L in registers
+constexpr bool kNoLdsTL = true;
+#else
+constexpr bool kNoLdsTL = false;
+#endif
+RT_D void tl_store(double* s_tl, V3 T, V3 L) {
+    const uint32_t l = stack_lane();
+    s_tl[l] = T.x; s_tl[kWave + l] = T.y; s_tl[2 * kWave + l] = T.z;
+    s_tl[3 * kWave + l] = L.x; s_tl[4 * kWave + l] = L.y; s_tl[5 * kWave + l] = L.z;
+}
+RT_D void tl_load(const double* s_tl, V3& T, V3& L) {
+    const uint32_t l = stack_lane();
+    T = v3(s_tl[l], s_tl[kWave + l], s_tl[2 * kWave + l]);
+    L = v3(s_tl[3 * kWave + l], s_tl[4 * kWave + l], s_tl[5 * kWave + l]);
+}
+
 template <bool ST, bool HIT, int WAVES, bool RES, int KM = 3, bool CMP = false>
-__global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams Pv,
+__global__ __launch_bounds__(kWave, (RES && WAVES == 4) ? kResOcc : WAVES) void path_kernel(DevScene Sv, KParams Pv,
                                                      const DevScene* __restrict__ Sg,
                                                      const KParams* __restrict__ Pg, double* __restrict__ out,
                                                      double* __restrict__ part, int32_t* __restrict__ hit_ids,
                                                      unsigned long long* __restrict__ stats, uint32_t* spill_n,
                                                      double* spill_t, uint32_t* __restrict__ queue,
                                                      double* __restrict__ ring_all) {
-    __shared__ uint32_t s_n[kShort * kWave];
-    __shared__ double s_t[kShort * kWave];
+    // the 4-wave resumable kernel: a shorter LDS stack, and the path's throughput and
+    // radiance in LDS (kTL) — they are read only while a lane shades, so they do not
+    // occupy registers (or scratch, where the 128-VGPR budget put them) across the
+    // triangle traversal
+    constexpr int kS = (RES && WAVES == 4) ? kShortRes : kShort;
+    constexpr bool kTL = RES && WAVES == 4 && !kNoLdsTL;
+    __shared__ uint32_t s_n[kS * kWave];
+    __shared__ double s_t[kS * kWave];
+    __shared__ double s_tl[kTL ? 6 * kWave : 1];  // [T.x T.y T.z L.x L.y L.z][lane]
     __shared__ uint32_t s_cnt[kRing];  // finished paths per ring row
     // camera rays of the next kCamSlots paths, [component][slot] (fused kernel only)
     __shared__ double s_cam[RES ? 1 : 3 * kCamSlots];
@@ -1337,8 +1369,8 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
     __shared__ double s_sum[3 * kWave];
 #endif
     const uint32_t lane = threadIdx.x;
-    auto stk = make_stack<RES>(s_n, s_t, 0u, (uint64_t)blockIdx.x * kWave, spill_n, spill_t,
-                           gridDim.x * kWave);
+    auto stk = make_stack<RES, kS>(s_n, s_t, 0u, (uint64_t)blockIdx.x * kWave, spill_n, spill_t,
+                                   gridDim.x * kWave);
     double* ring = ring_all + (uint64_t)blockIdx.x * kRing * kWave * 3;
     const KParams& Pt = WAVES == 3 ? *Pg : Pv;  // per-wave-tile constants
     const uint32_t depth = Pt.ray_depth;
@@ -1455,8 +1487,12 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
                     } else {
                         ps.d = camera_dir(P, px, py, rng);
                     }
-                    ps.T = v3(1.0, 1.0, 1.0);
-                    ps.L = v3(0.0, 0.0, 0.0);
+                    if constexpr (kTL) {
+                        tl_store(s_tl, v3(1.0, 1.0, 1.0), v3(0.0, 0.0, 0.0));
+                    } else {
+                        ps.T = v3(1.0, 1.0, 1.0);
+                        ps.L = v3(0.0, 0.0, 0.0);
+                    }
                     ps.pend = false;
                     b = 0;
                     busy = true;
@@ -1500,7 +1536,15 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
                 if (inq) {
                     int32_t g;
                     const unsigned long long ph_s = PH_T();
+                    if constexpr (kTL) {
+                        tl_load(s_tl, ps.T, ps.L);
+                        rng_rekey(rng, P.seed);
+                    }
                     cont = segment_end<ST, KM, CMP>(S, P, sc, ps, rng, stk, C, q, g, b + 1 >= depth);
+                    if constexpr (kTL) {
+                        tl_store(s_tl, ps.T, ps.L);
+                        rng_park(rng);
+                    }
                     PH_ADDW(kPhSegment, ph_s);
                     if (HIT) hit_ids[(pixel * P.spp + s) * depth + b] = g;
                     ++b;
@@ -1525,6 +1569,7 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
             if (HIT) for (uint32_t k = b; k < depth; ++k) hit_ids[(pixel * P.spp + s) * depth + k] = RT_HIT_NONE;
             const uint32_t r = (cur / kWave) % kRing;
             double* rp = ring + ((uint64_t)r * kWave + cur % kWave) * 3;
+            if constexpr (kTL) { V3 t; tl_load(s_tl, t, ps.L); }
             rp[0] = ps.L.x; rp[1] = ps.L.y; rp[2] = ps.L.z;
             atomicAdd(&s_cnt[r], 1u);
             busy = false;

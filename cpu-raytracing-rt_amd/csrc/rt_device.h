@@ -103,6 +103,18 @@ RT_D void rng_top_up(Rng& r) {  // coherent refill point (see Rng)
 // every hit (oracle.c rng_align), so all lanes start their shading draws on a
 // block boundary and lanes in the same branch refill at the same points.
 RT_D void rng_align(Rng& r) { r.avail = 0; }
+// Between two shading steps of the resumable path kernel a stream needs only its
+// counter: the next shading step starts with rng_align, so the buffered words
+// are never read (avail = 0), and a next block computed ahead (nready) is
+// dropped and recomputed later from the same counter (blk - 1) — the same words.
+// The key is re-read from the frame constants (rng_rekey) before the next step.
+// Then nothing of the stream but blk (and its pixel / sample) stays live in
+// registers across the triangle traversal.
+RT_D void rng_park(Rng& r) {
+    if (r.nready) { r.blk--; r.nready = 0; }
+    r.avail = 0;
+}
+RT_D void rng_rekey(Rng& r, uint64_t seed) { r.k0 = (uint32_t)seed; r.k1 = (uint32_t)(seed >> 32); }
 RT_D uint32_t next_u32(Rng& r) {
     if (r.avail == 0) {
         if (!r.nready) philox_next(r);

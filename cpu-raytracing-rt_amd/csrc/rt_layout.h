@@ -20,6 +20,13 @@ namespace rt {
 #define RT_SHORT_STACK 12
 #endif
 constexpr int kMaxBvhDepthShort = RT_SHORT_STACK;   // per-lane short stack kept in LDS
+// The 4-wave resumable path kernel's short stack: shorter, so the path's
+// throughput and radiance fit in its LDS too (render.hip path_kernel)
+#ifndef RT_SHORT_STACK_RES
+#define RT_SHORT_STACK_RES 8
+#endif
+constexpr int kShortRes = RT_SHORT_STACK_RES;
+constexpr int kMinShort = kShortRes < kMaxBvhDepthShort ? kShortRes : kMaxBvhDepthShort;  // spill sizing
 
 struct alignas(128) DevNode {
     double lmin[3], lmax[3];   // left child's box  (bvh.rs:158)
