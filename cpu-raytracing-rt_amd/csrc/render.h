@@ -86,11 +86,14 @@ struct PathWork {
 constexpr uint32_t kRingRows = RT_RING_ROWS;   // render.hip kRing (power of two, <= 64)
 // Suspend threshold of the resumable triangle traversal (path_kernel RES): fewer
 // live lanes than this and the wave lets its waiting lanes shade and start new
-// rays.  A cache-resident BVH (C3, ~40 MB) runs best at 24 (16: +0.3%, 32: +3.7%);
+// rays.  A cache-resident BVH (C3, ~40 MB) ran best at 24 in round 2 (16: +0.3%,
+// 32: +3.7%); with the path's T and L in LDS a suspension costs less (no spill
+// traffic per trip) and 32 wins (C3 203.8 -> 201.1 ms at 64 spp, 16: +4.9%;
+// profiles/r03/variants/variants_suspend_tl_C3.log, variants_suspend32_C3.log: 28 +0.3%, 36 +0.4%, 40 +2.4%, 48 +7.9%);
 // one that streams from HBM (C5, ~1.4 GB, past the 256-MiB Infinity Cache) at 40
 // (16: +16.6%, 24: +5.3%, 48: +1.6%; profiles/r02/variants/variants_suspend*.log):
 // there every lane sent back to issue its next ray adds memory-level parallelism.
-constexpr uint32_t kSuspendCached = 24, kSuspendStreamed = 40;
+constexpr uint32_t kSuspendCached = 32, kSuspendStreamed = 40;
 // Leaf batch of the same kernel (lanes waiting at leaves before the wave tests
 // them): C3 16 -> 32 lanes 236.3 -> 227.1 ms, C5 16 -> 24 lanes 260.3 -> 249.5 ms at
 // 64 spp (profiles/r02/variants/variants_leaflanes*.log).

@@ -332,7 +332,11 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
         PH_COUNT(kPhInnerWave, kPhInnerLane);
         const float4* nw = (const float4*)(B.cnodes + T.node);
         const float4 w0 = nw[0], w1 = nw[1], w2 = nw[2];
+#ifndef RT_NODE_K4  // the two child words only (56 of the 64 B: a leaf's own range is read by trav_enter)
+        const uint2 k = ((const uint2*)nw)[6];
+#else  // ablation build: the whole fourth 16-B word
         const uint4 k = ((const uint4*)nw)[3];
+#endif
         asm volatile("" ::"v"(w1.z), "v"(w1.w), "v"(w2.x), "v"(w2.y), "v"(w2.z), "v"(w2.w));  // see node_boxes
         double lt = 0.0, rt2 = 0.0;
         C.aabb(2);

@@ -103,11 +103,6 @@ for s in $STEPS; do
       run calib_dram 120 rocprofv3 --pmc TCC_EA0_RDREQ_DRAM_sum TCC_HIT_sum TCC_MISS_sum --output-format csv \
         -d "$OUT/calib_dram" -o run -- tools/fetch_calib || exit 1
       run calib_report 60 python3 tools/fetch_calib.py "$OUT" || exit 1 ;;
-    pcs2|pcs3|pcs5)  # host-trap PC sampling of the path kernel (where its wave-time goes, per instruction)
-      w=C${s#pcs}
-      run pcs_$w 420 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method host_trap --pc-sampling-unit time \
-        --pc-sampling-interval ${PCS_INTERVAL:-1} --output-format csv -d "$OUT/pcs_$w" -o run \
-        -- $B --workload $w --spp ${PCS_SPP:-16} --steps 1 --warmup 0 --no-cpu-baseline --no-pmc || exit 1 ;;
   esac
 done
 echo "[$(date +%T)] batch done"
