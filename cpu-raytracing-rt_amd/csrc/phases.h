@@ -16,7 +16,9 @@ namespace rt {
 enum { kPhAssign, kPhIntersect, kPhLightSample, kPhLightPdf, kPhSegment, kPhCommit, kPhTile,
        kPhTravWave, kPhTravLane, kPhLeafWave, kPhLeafLane, kPhRngWave, kPhRngLane, kPhW0,
        kPhPlanes = kPhW0 + 5, kPhBoxes, kPhElls, kPhTris, kPhMaterialise,
-       kPhInnerWave, kPhInnerLane, kPhLiveLane, kPhRngFallWave, kPhRngFallLane, kPhN };
+       kPhInnerWave, kPhInnerLane, kPhLiveLane, kPhRngFallWave, kPhRngFallLane,
+       kPhPushLane, kPhPushGlobal, kPhPopGlobal, kPhN };  // traversal-stack pushes, past the LDS part
+static_assert(16 + kPhN <= 48, "phase words fit the raw stats");
 constexpr int kPhW = kPhW0 - kPhIntersect;  // weighted word of region k = k + kPhW (k in 1..5)
 #ifdef RT_PHASES
 __shared__ unsigned long long g_phase[kPhN];

@@ -63,8 +63,12 @@ struct Stack {
     RT_D uint32_t lane() const { return OPQ ? stack_lane() : ln; }
     RT_D void push(uint32_t node, double t) {
         const uint32_t l = lane();
+        PH_LANE(kPhPushLane);
         if (sp < KS) { sn[sp * kWave + l] = node; st[sp * kWave + l] = t; }
-        else { gn[(size_t)(sp - KS) * stride + l] = node; gt[(size_t)(sp - KS) * stride + l] = t; }
+        else {
+            PH_LANE(kPhPushGlobal);
+            gn[(size_t)(sp - KS) * stride + l] = node; gt[(size_t)(sp - KS) * stride + l] = t;
+        }
         ++sp;
     }
     // The spill side reads through volatile pointers: otherwise the compiler
@@ -75,6 +79,7 @@ struct Stack {
         const uint32_t l = lane();
         if (sp < KS) { node = sn[sp * kWave + l]; t = st[sp * kWave + l]; }
         else {
+            PH_LANE(kPhPopGlobal);
             node = ((volatile const uint32_t*)gn)[(size_t)(sp - KS) * stride + l];
             t = ((volatile const double*)gt)[(size_t)(sp - KS) * stride + l];
         }

@@ -533,8 +533,26 @@ RT_D bool tri_uvt_r(const TriRec& r, V3 o, V3 d, double& u, double& v, double& t
     double det = m0.x * (m1.y * m2.z - m2.y * m1.z) - m1.x * (m0.y * m2.z - m2.y * m0.z) +
                  m2.x * (m0.y * m1.z - m1.y * m0.z);
     if (fabs(det) < 1e-11) return false;
-    auto dv = [&](V3 c) { return c / det; };
-    V3 x0 = dv(cross(m1, m2)), x1 = dv(cross(m2, m0)), x2 = dv(cross(m0, m1));
+    const V3 c0 = cross(m1, m2), c1 = cross(m2, m0), c2 = cross(m0, m1);
+    V3 x0, x1, x2;
+#ifdef RT_TRI_QUOT
+    // The nine quotients c / det by the split division (dev_rcp once, dev_quotz per
+    // component): the same bits as c / det when det is in dir_ok's range and every
+    // dividend is 0 or in [2^-500, 2^402] (see "exact division"); taken when every
+    // lane testing a triangle here satisfies it, the plain division otherwise.
+    auto qok = [](double x) { const double a = fabs(x); return x == 0.0 || (a >= 0x1p-500 && a <= 0x1p402); };
+    const bool ok = dir_ok(det) && qok(c0.x) && qok(c0.y) && qok(c0.z) && qok(c1.x) && qok(c1.y) && qok(c1.z) &&
+                    qok(c2.x) && qok(c2.y) && qok(c2.z);
+    if (__ballot(!ok) == 0) {
+        const double rd = dev_rcp(det);
+        auto dq = [&](V3 c) { return v3(dev_quotz(c.x, det, rd), dev_quotz(c.y, det, rd), dev_quotz(c.z, det, rd)); };
+        x0 = dq(c0); x1 = dq(c1); x2 = dq(c2);
+    } else
+#endif
+    {
+        auto dv = [&](V3 c) { return c / det; };
+        x0 = dv(c0); x1 = dv(c1); x2 = dv(c2);
+    }
     V3 w = o - r.a;
     double uu = dot(x0, w), vv = dot(x1, w), tt = dot(x2, w);
     if (uu < 0.0 || vv < 0.0 || 1.0 < uu + vv || tt < 0.0) return false;

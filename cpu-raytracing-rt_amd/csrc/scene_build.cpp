@@ -317,7 +317,37 @@ void build_compact(const HostBvh& h, const std::vector<TriItem>& items, HostBvhA
         if (!f32_exact3(n.box.min) || !f32_exact3(n.box.max)) return;
     for (const TriItem& it : items)
         if (!f32_exact3(it.t.a) || !f32_exact3(it.b) || !f32_exact3(it.c)) return;
-    std::vector<DevNodeC> cn(h.nodes.size());
+    // Record slots.  Pre-order (the reference's numbering, bvh.rs:104): a node and
+    // its left child share a 128-B line half the time.  RT_SIBLING_PAIRS
+    // (experiment): the two children of a node share one line (slots 2k, 2k + 1),
+    // pairs allocated in pre-order, so a far child popped after its sibling's
+    // subtree finds its record in the line the near descent fetched.  Only the
+    // addresses differ: the child words carry the slots, the root stays slot 0.
+    std::vector<uint32_t> slot(h.nodes.size());
+    size_t n_slots = h.nodes.size();
+#ifdef RT_SIBLING_PAIRS
+    {
+        uint32_t next = 2;  // slot 1 pads the root's line
+        slot[0] = 0;
+        std::vector<uint32_t> st{0};
+        while (!st.empty()) {
+            const uint32_t i = st.back();
+            st.pop_back();
+            const HostNode& n = h.nodes[i];
+            if (n.left < 0) continue;
+            slot[n.left] = next; slot[n.right] = next + 1;
+            next += 2;
+            st.push_back((uint32_t)n.right);
+            st.push_back((uint32_t)n.left);
+        }
+        n_slots = next;
+    }
+#else
+    for (size_t i = 0; i < h.nodes.size(); ++i) slot[i] = (uint32_t)i;
+#endif
+    if (n_slots >= kLeafRef) return;
+    std::vector<DevNodeC> cn(n_slots);
+    std::memset(cn.data(), 0, n_slots * sizeof(DevNodeC));
     auto put3 = [](float* d, V3 v) { d[0] = (float)v.x; d[1] = (float)v.y; d[2] = (float)v.z; };
     for (size_t i = 0; i < h.nodes.size(); ++i) {
         const HostNode& n = h.nodes[i];
@@ -326,15 +356,14 @@ void build_compact(const HostBvh& h, const std::vector<TriItem>& items, HostBvhA
         if (n.left >= 0) {
             const HostNode& l = h.nodes[n.left];
             const HostNode& r = h.nodes[n.right];
-            if ((uint64_t)n.left != i + 1) return;  // pre-order: the left child follows its parent
             put3(c.lmin, l.box.min); put3(c.lmax, l.box.max);
             put3(c.rmin, r.box.min); put3(c.rmax, r.box.max);
-            c.lw = child_word((uint32_t)n.left, (uint32_t)l.start, (uint32_t)(l.end - l.start));
-            c.rw = child_word((uint32_t)n.right, (uint32_t)r.start, (uint32_t)(r.end - r.start));
+            c.lw = child_word(slot[n.left], (uint32_t)l.start, (uint32_t)(l.end - l.start));
+            c.rw = child_word(slot[n.right], (uint32_t)r.start, (uint32_t)(r.end - r.start));
         }
         c.start = (uint32_t)n.start;
         c.count = (uint32_t)(n.end - n.start);
-        cn[i] = c;
+        cn[slot[i]] = c;
     }
     std::vector<float> ct(items.size() * kTriC);
     for (size_t k = 0; k < h.order.size(); ++k) {

@@ -21,7 +21,8 @@ NAMES = ["assign", "intersect", "light_sample", "light_pdf", "segment", "commit"
          "rng_wave_refills", "rng_lane_refills",
          "w_intersect", "w_light_sample", "w_light_pdf", "w_segment", "w_commit",
          "isect_planes", "isect_boxes", "isect_ellipsoids", "isect_triangles", "isect_materialise",
-         "inner_wave_iters", "inner_lane_iters", "live_lane_iters", "rng_fallback_wave", "rng_fallback_lane"]
+         "inner_wave_iters", "inner_lane_iters", "live_lane_iters", "rng_fallback_wave", "rng_fallback_lane",
+         "push_lane", "push_global", "pop_global"]
 rt = load_package()
 wl = sys.argv[1]
 scene_file, W, H, spp, depth = bench.WORKLOADS[wl]
@@ -49,6 +50,9 @@ print(json.dumps({"workload": wl, "spp": spp, "segments": st["segments"],
                   "rng_refill_util": ph["rng_lane_refills"] / max(1, 64 * ph["rng_wave_refills"]),
                   "rng_wave_refills_per_segment": ph["rng_wave_refills"] * 64 / max(1, st["segments"]),
                   "rng_fallback_share": ph["rng_fallback_wave"] / max(1, ph["rng_wave_refills"]),
+                  "stack_pushes_per_segment": ph["push_lane"] / max(1, st["segments"]),
+                  "global_push_share": ph["push_global"] / max(1, ph["push_lane"]),
+                  "global_stack_bytes": 12 * (ph["push_global"] + ph["pop_global"]),
                   "region_entry_lane_util": {k: round(ph["w_" + k] / max(1, ph[k]), 4)
                                              for k in ("intersect", "light_sample", "light_pdf", "segment")},
                   "wave_cycles": ph, "share_of_tile_time": {k: round(v, 4) for k, v in share.items()}}))
