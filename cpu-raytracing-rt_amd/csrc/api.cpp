@@ -676,6 +676,23 @@ int rt_intersect_rays(rt_scene* s, const double* rays, uint32_t n, rt_hit* out) 
 int rt_intersect_rays_async(rt_scene* s, const double* d_rays, uint32_t n, rt_hit* d_out, int method,
                             void* hip_stream) {
     if (!s || (!d_rays && n) || (!d_out && n)) return set_error(RT_ERR_INVALID, "bad arguments");
+#ifdef RT_WF_PROBE
+    if (method == 2) {  // experiment: the traversal-only kernel (render.hip trace_tri_kernel)
+        if (n == 0) return RT_OK;
+        DEVICE_GUARD(s);
+        if (!s->dev.tris.cnodes || path_kinds(s) != 2) return set_error(RT_ERR_INVALID, "probe: compact triangles only");
+        uint32_t grid = 0;
+        HIP_TRY(trace_tri_grid(n, &grid));
+        int rc = ensure_spill(s, (uint64_t)grid * 64);
+        if (rc) return rc;
+        if (!s->queue) HIP_TRY(hipMalloc(&s->queue, kQueueWords * sizeof(uint32_t)));
+        const hipStream_t st = (hipStream_t)hip_stream;
+        HIP_TRY(ws_begin(s, st));
+        HIP_TRY(launch_trace_tri(s->dev, d_rays, n, d_out, s->queue, s->spill_n, s->spill_t, grid, st));
+        HIP_TRY(ws_end(s, st));
+        return RT_OK;
+    }
+#endif
     if (method != RT_TRACE_PER_RAY && method != RT_TRACE_PERSISTENT) return set_error(RT_ERR_INVALID, "bad method");
     if (n == 0) return RT_OK;
     DEVICE_GUARD(s);

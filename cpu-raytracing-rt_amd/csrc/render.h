@@ -110,6 +110,11 @@ hipError_t launch_reduce_chunks(const double* part, double* out, const KParams& 
 hipError_t launch_trace(const DevScene& S, const double* rays, uint32_t n, rt_hit* out, uint32_t* queue,
                         uint32_t* spill_n, double* spill_t, uint32_t grid, bool compact, hipStream_t st);
 hipError_t trace_grid(uint32_t n, uint32_t* grid);
+#ifdef RT_WF_PROBE
+hipError_t launch_trace_tri(const DevScene& S, const double* rays, uint32_t n, rt_hit* out, uint32_t* queue,
+                            uint32_t* spill_n, double* spill_t, uint32_t grid, hipStream_t st);
+hipError_t trace_tri_grid(uint32_t n, uint32_t* grid);
+#endif
 hipError_t launch_intersect(const DevScene& S, const double* rays, uint32_t n, rt_hit* out, uint32_t* spill_n,
                             double* spill_t, hipStream_t st);
 hipError_t launch_light(const DevScene& S, const double* rays, uint32_t n, int mode, double* out, uint32_t* cnt,

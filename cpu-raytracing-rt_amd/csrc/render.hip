@@ -281,6 +281,17 @@ RT_D TriRec load_tri_c(const float* __restrict__ p) {
     return TriRec{A, v3(b.x, b.y, b.z) - A, v3(c.x, c.y, c.z) - A};
 }
 
+// the same record as its nine floats (a prefetch that holds 9 VGPRs, widened later)
+struct F9 { F3 a, b, c; };
+RT_D F9 load_f9(const float* __restrict__ p) {
+    const F3* q = (const F3*)p;
+    return F9{q[0], q[1], q[2]};
+}
+RT_D TriRec widen_f9(const F9& r) {
+    const V3 A = v3(r.a.x, r.a.y, r.a.z);
+    return TriRec{A, v3(r.b.x, r.b.y, r.b.z) - A, v3(r.c.x, r.c.y, r.c.z) - A};
+}
+
 #ifdef RT_RECOMPUTE_UV  // experiment: the compact kernel re-tests the winner for (u, v) instead of carrying them
 constexpr bool kRecomputeUV = true;
 #else
@@ -304,6 +315,37 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
                 // Software-pipelined leaf: the next triangle's record loads while this one
                 // is tested (C3 -0.8%, C5 -1.0% at reduced spp, variants_leafpipe_*.log).
                 const uint32_t end = T.start + T.cnt;
+#ifndef RT_LEAF_PIPE_CMP  // ablation build: the compact records software-pipelined too
+                if constexpr (CMP) {
+                    // Compact records are loaded when tested: the pipelined form holds the
+                    // next record widened (18 VGPRs) through the test, which the 4-wave
+                    // kernel pays in spills (a traversal-only kernel needs 105 VGPRs with it,
+                    // 84 without): C3 -0.9%, C5 -1.9% at reduced spp
+                    // (profiles/r03/variants/variants_leafpipe_C*.log).  RT_LEAF_RAWPIPE:
+                    // prefetch the next record as its nine floats (C3 -0.4%, C5 -2.1%).
+#ifdef RT_LEAF_RAWPIPE
+                    F9 nraw = load_f9(B.ctris + (size_t)T.start * kTriC);
+#endif
+                    for (uint32_t i = T.start; i < end; ++i) {
+                        PH_COUNT(kPhLeafWave, kPhLeafLane);
+#ifdef RT_LEAF_RAWPIPE
+                        const F9 craw = nraw;
+                        if (i + 1 < end) nraw = load_f9(B.ctris + (size_t)(i + 1) * kTriC);
+                        const TriRec cur = widen_f9(craw);
+#else
+                        const TriRec cur = load_tri_c(B.ctris + (size_t)i * kTriC);
+#endif
+                        double t, u = 0.0, v = 0.0;
+                        C.tri();
+                        const bool h = tri_uvt_r(cur, o, d, u, v, t);
+                        if (h && (!T.valid || t < T.best)) {  // update_best_intersection (bvh.rs:213-222)
+                            T.valid = true; T.best = t; T.prim = i; T.aux = 0;
+                            if (!kRecomputeUV) { T.bu = u; T.bv = v; }
+                        }
+                    }
+                } else
+#endif
+                {
                 TriRec cur = CMP ? load_tri_c(B.ctris + (size_t)T.start * kTriC) : load_tri(B.tris[T.start]);
                 for (uint32_t i = T.start; i < end; ++i) {
                     PH_COUNT(kPhLeafWave, kPhLeafLane);
@@ -317,6 +359,7 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
                         if (!(CMP && kRecomputeUV)) { T.bu = u; T.bv = v; }
                     }
                     cur = nxt;
+                }
                 }
             } else
 #endif
@@ -1875,6 +1918,86 @@ hipError_t launch_trace(const DevScene& S, const double* rays, uint32_t n, rt_hi
         hipLaunchKernelGGL(trace_kernel<4>, dim3(grid), dim3(kWave), 0, st, S, rays, n, out, queue, spill_n, spill_t);
     return hipGetLastError();
 }
+#ifdef RT_WF_PROBE
+// Experiment (variant builds only): a traversal-only persistent kernel for a
+// triangle-only scene on the compact layout — the trace half of a wavefront form.
+// It carries only the ray, its reciprocals and the traversal state, so it may run
+// more waves per SIMD (RT_WF_WAVES) with a KS-entry LDS stack.  Writes t and the
+// global id of the closest triangle (rt_hit.t / .prim; the normals are not filled).
+#ifndef RT_WF_WAVES
+#define RT_WF_WAVES 6
+#endif
+constexpr int kWfKS = 8;
+template <int WAVES, int KS>
+__global__ __launch_bounds__(kWave, WAVES) void trace_tri_kernel(DevScene S, const double* __restrict__ rays,
+                                                                 uint32_t n, rt_hit* __restrict__ out,
+                                                                 uint32_t* __restrict__ queue, uint32_t* spill_n,
+                                                                 double* spill_t) {
+    __shared__ uint32_t s_n[KS * kWave];
+    __shared__ double s_t[KS * kWave];
+    auto stk = make_stack<true, KS>(s_n, s_t, 0u, (uint64_t)blockIdx.x * kWave, spill_n, spill_t, gridDim.x * kWave);
+    Cnt<false> C;
+    const uint64_t below = (1ull << threadIdx.x) - 1ull;
+    bool has = false, drained = false;
+    uint32_t idx = 0;
+    V3 o = v3(0, 0, 0), d = v3(0, 0, 0);
+    Rcp3 rc;
+    bool fast = false;
+    Trav T;
+    T.live = false;
+    for (;;) {
+        const uint64_t idle = __ballot(!has);
+        const uint64_t lv = __ballot(T.live);
+        if (!drained && idle && (__popcll(idle) >= kRefill || lv == 0)) {
+            uint32_t b = 0;
+            if (threadIdx.x == 0) b = atomicAdd(queue, (uint32_t)__popcll(idle));
+            const uint32_t base = __builtin_amdgcn_readfirstlane(b);
+            if ((uint64_t)base + (uint64_t)__popcll(idle) >= n) drained = true;
+            if (!has) {
+                const uint32_t k = base + (uint32_t)__popcll(idle & below);
+                if (k < n) {
+                    idx = k;
+                    o = load3(rays + 6 * (size_t)k);
+                    d = load3(rays + 6 * (size_t)k + 3);
+                    rc = make_rcp3(d);
+                    fast = S.tris.fast && ray_fast(o, rc);
+                    trav_init<2, false>(S.tris, o, d, rc, fast, stk, C, T);
+                    has = true;
+                }
+            }
+        }
+        const uint64_t lv2 = __ballot(T.live);
+        if (lv2) trav_step<3, 2, false, true>(S.tris, o, d, rc, fast, stk, C, T, lv2, 32);
+        if (has && !T.live) {
+            rt_hit* r = out + idx;
+            r->t = T.valid ? T.best : 0.0;
+            r->prim = T.valid ? S.tris.gid[T.prim] : RT_HIT_MISS;
+            has = false;
+        }
+        if (drained && !__ballot(has)) break;
+    }
+}
+hipError_t launch_trace_tri(const DevScene& S, const double* rays, uint32_t n, rt_hit* out, uint32_t* queue,
+                            uint32_t* spill_n, double* spill_t, uint32_t grid, hipStream_t st) {
+    hipError_t e = hipMemsetAsync(queue, 0, kQueueWords * sizeof(uint32_t), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((trace_tri_kernel<RT_WF_WAVES, kWfKS>), dim3(grid), dim3(kWave), 0, st, S, rays, n, out, queue,
+                       spill_n, spill_t);
+    return hipGetLastError();
+}
+hipError_t trace_tri_grid(uint32_t n, uint32_t* grid) {
+    int dev = 0, cus = 0, per_cu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e == hipSuccess)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)trace_tri_kernel<RT_WF_WAVES, kWfKS>,
+                                                         kWave, 0);
+    if (e != hipSuccess) return e;
+    const uint64_t g = (uint64_t)std::max(per_cu, 1) * (uint64_t)std::max(cus, 1);
+    *grid = (uint32_t)std::min<uint64_t>(g, std::max<uint64_t>(((uint64_t)n + kWave - 1) / kWave, 1));
+    return hipSuccess;
+}
+#endif
 hipError_t trace_grid(uint32_t n, uint32_t* grid) {
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
