@@ -292,6 +292,53 @@ RT_D TriRec widen_f9(const F9& r) {
     return TriRec{A, v3(r.b.x, r.b.y, r.b.z) - A, v3(r.c.x, r.c.y, r.c.z) - A};
 }
 
+// Quad-shared node loads (RT_QUAD_NODE).  Scattered rays make every lane of a
+// 16-B load its own cache-line request: four per lane and node visit, the texture
+// addresser's work (TA busy 93% on C3).  Here the four lanes of a quad
+// load the four 16-B words of ONE lane's node per round (one line per quad, 16 per
+// wave-instruction instead of 64), for the quad's four lanes in turn, then a 4x4
+// transpose of 16-B words inside the quad (two DPP butterfly steps) gives each lane
+// its own node's words.  The same bytes reach the same lanes.
+#ifdef RT_QUAD_NODE
+constexpr bool kQuadNode = true;
+template <int CTRL>
+RT_D uint32_t dppq(uint32_t v) { return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xF, 0xF, false); }
+template <int CTRL>
+RT_D uint4 dppq4(uint4 v) { return make_uint4(dppq<CTRL>(v.x), dppq<CTRL>(v.y), dppq<CTRL>(v.z), dppq<CTRL>(v.w)); }
+RT_D uint4 sel4(bool c, uint4 a, uint4 b) { return c ? a : b; }
+RT_D float4 u4f(uint4 v) {
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+RT_D void quad_node_load(const DevNodeC* __restrict__ nodes, uint32_t node, bool inner, uint4& y0, uint4& y1,
+                         uint4& y2, uint4& y3) {
+    const uint32_t lane = stack_lane();
+    const uint32_t qi = lane & 3u;
+    const uint64_t im = __ballot(inner) >> (lane & ~3u);  // bit r: the quad's lane r is at an inner node
+    const uint4* base = (const uint4*)nodes;
+    uint4 x[4];
+    const uint32_t n0 = dppq<0x00>(node), n1 = dppq<0x55>(node), n2 = dppq<0xAA>(node), n3 = dppq<0xFF>(node);
+    // round r: word qi of the node of the quad's lane r (quad_perm broadcast of its index)
+    x[0] = (im & 1u) ? base[(size_t)n0 * 4 + qi] : make_uint4(0, 0, 0, 0);
+    x[1] = (im & 2u) ? base[(size_t)n1 * 4 + qi] : make_uint4(0, 0, 0, 0);
+    x[2] = (im & 4u) ? base[(size_t)n2 * 4 + qi] : make_uint4(0, 0, 0, 0);
+    x[3] = (im & 8u) ? base[(size_t)n3 * 4 + qi] : make_uint4(0, 0, 0, 0);
+    // lane i slot r = word i of node(r) -> word r of node(i): swap with lane i ^ 1 the
+    // slots whose bit 0 differs from i's, then with lane i ^ 2 those whose bit 1 does
+    const bool odd = qi & 1u, hi = qi & 2u;
+    {
+        const uint4 r0 = dppq4<0xB1>(sel4(odd, x[0], x[1])), r1 = dppq4<0xB1>(sel4(odd, x[2], x[3]));
+        if (odd) { x[0] = r0; x[2] = r1; } else { x[1] = r0; x[3] = r1; }
+    }
+    {
+        const uint4 r0 = dppq4<0x4E>(sel4(hi, x[0], x[2])), r1 = dppq4<0x4E>(sel4(hi, x[1], x[3]));
+        if (hi) { x[0] = r0; x[1] = r1; } else { x[2] = r0; x[3] = r1; }
+    }
+    y0 = x[0]; y1 = x[1]; y2 = x[2]; y3 = x[3];
+}
+#else
+constexpr bool kQuadNode = false;
+#endif
+
 #ifdef RT_RECOMPUTE_UV  // experiment: the compact kernel re-tests the winner for (u, v) instead of carrying them
 constexpr bool kRecomputeUV = true;
 #else
@@ -376,8 +423,18 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
             }
             next = true;
         }
-    } else if (CMP && T.live && T.cnt == 0) {  // internal node, compact layout (one 64-B half line)
-        PH_COUNT(kPhInnerWave, kPhInnerLane);
+    } else if (CMP && (kQuadNode || (T.live && T.cnt == 0))) {  // internal node, compact layout (64 B)
+#ifdef RT_QUAD_NODE
+        // Quad-shared node loads: the whole wave is here (do_leaves is uniform); see
+        // quad_node_load.  Lanes not at an inner node take part in their quad's loads.
+        const bool inner = T.live && T.cnt == 0;
+        uint4 q0, q1, q2, q3;
+        quad_node_load(B.cnodes, T.node, inner, q0, q1, q2, q3);
+        if (inner) {
+        const float4 w0 = u4f(q0), w1 = u4f(q1), w2 = u4f(q2);
+        const uint2 k = make_uint2(q3.x, q3.y);
+#else
+        {
         const float4* nw = (const float4*)(B.cnodes + T.node);
         const float4 w0 = nw[0], w1 = nw[1], w2 = nw[2];
 #ifndef RT_NODE_K4  // the two child words only (56 of the 64 B: a leaf's own range is read by trav_enter)
@@ -386,6 +443,8 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
         const uint4 k = ((const uint4*)nw)[3];
 #endif
         asm volatile("" ::"v"(w1.z), "v"(w1.w), "v"(w2.x), "v"(w2.y), "v"(w2.z), "v"(w2.w));  // see node_boxes
+#endif
+        PH_COUNT(kPhInnerWave, kPhInnerLane);
         double lt = 0.0, rt2 = 0.0;
         C.aabb(2);
         const bool lh = slab_v<SLAB>(v3(w0.x, w0.y, w0.z), v3(w0.w, w1.x, w1.y), o, d, rc, fast, lt);
@@ -401,6 +460,7 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
             } else go_left = true;
         } else if (!(ri < bt)) next = true;
         if (!next) trav_enter<true>(B, T, go_left ? k.x : k.y);
+        }
     } else if (!CMP && T.live && T.cnt == 0) {  // internal node (count 0 <=> children)
         PH_COUNT(kPhInnerWave, kPhInnerLane);
         const DevNode& n = B.nodes[T.node];
