@@ -338,6 +338,8 @@ def main():
     # untimed counting pass: this rank's work of one frame
     scene.read_stats(reset=True)
     scene.render_tiles_async(params, rank, part, tiles.data_ptr(), sptr, stats=True)
+    torch.cuda.synchronize()
+    lq_skipped = int(scene.read_raw_stats(11)[10])  # last-bounce light queries the timed kernel skips
     st = scene.read_stats(reset=True)
     seg = torch.tensor([st["segments"], st["paths"]], dtype=torch.float64, device=dev)
     if world > 1:
@@ -410,7 +412,10 @@ def main():
             # cache-level throughput, not an HBM one, and is not used as `frac`
             "algorithmic": {"bytes_per_launch": algo, "GBps": algo / kern_s / 1e9,
                             "model": "32*aabb_tests + 72*tri_tests + 80*shape_tests + 100*shaded_hits "
-                                     "(rank 0 tiles)"},
+                                     "(rank 0 tiles)",
+                            # counted by the stats instance, which also runs the last-bounce light
+                            # queries the timed kernel proves NaN-free and skips
+                            "light_queries": st["light_queries"], "light_queries_skipped": lq_skipped},
             "note": "bound = f64 VALU issue: frac = VALU busy SIMD-cycles / available (valu_detail); the "
                     "measured HBM rate is roofline.hbm (traffic = PMC HBM bytes per launch)",
         })

@@ -368,6 +368,38 @@ uint32_t slt_mask(const HostScene& hs) {
     return j == L.shapes.size() ? mask : 0;
 }
 
+// DevScene::lq_boxes / lq_box: the light boxes' world-space bounds (the eight
+// corners pos + rotate(rot, +-half sizes); model_ray maps world to model space by
+// the conjugate, so model to world is rot itself), grown by a margin of 1e-6 of
+// the coordinates' magnitude (+1e-100) that dwarfs the rounding of the rotation and
+// of the query's slab arithmetic.  Zero (no skipping) unless every light is a box,
+// there are at most kLqBoxes, and every box and density is finite and positive.
+uint32_t lq_boxes(const HostScene& hs, double (*out)[6]) {
+    const auto& L = hs.bvh[3].shapes;
+    if (L.empty() || L.size() > kLqBoxes || !hs.bvh[4].shapes.empty() || !hs.bvh[5].tris.empty()) return 0;
+    for (size_t i = 0; i < L.size(); ++i) {
+        const DevShape& b = L[i];
+        const double pb = b.aux[0];
+        if (!(pb > 0.0) || !std::isfinite(pb)) return 0;
+        const Quat q = load_quat(b.rot);
+        V3 lo = v3(INFINITY, INFINITY, INFINITY), hi = v3(-INFINITY, -INFINITY, -INFINITY);
+        for (int c = 0; c < 8; ++c) {
+            const V3 h = v3((c & 1) ? b.shape[0] : -b.shape[0], (c & 2) ? b.shape[1] : -b.shape[1],
+                            (c & 4) ? b.shape[2] : -b.shape[2]);
+            const V3 p = load3(b.pos) + rotate(q, h);
+            lo = v3(std::min(lo.x, p.x), std::min(lo.y, p.y), std::min(lo.z, p.z));
+            hi = v3(std::max(hi.x, p.x), std::max(hi.y, p.y), std::max(hi.z, p.z));
+        }
+        const double mag = std::max({std::fabs(lo.x), std::fabs(lo.y), std::fabs(lo.z), std::fabs(hi.x),
+                                     std::fabs(hi.y), std::fabs(hi.z)});
+        if (!std::isfinite(mag) || mag > 0x1p400) return 0;
+        const double m = 1e-6 * (1.0 + mag) + 1e-100;
+        const double v[6] = {lo.x - m, lo.y - m, lo.z - m, hi.x + m, hi.y + m, hi.z + m};
+        for (int k = 0; k < 6; ++k) out[i][k] = v[k];
+    }
+    return (uint32_t)L.size();
+}
+
 template <class T>
 struct DevBuf {  // RAII device buffer for per-call scratch
     T* p = nullptr;
@@ -455,6 +487,8 @@ int scene_upload(const HostScene& hs, rt_scene** out) {
     // UINT64_MAX - (2^64 - n) % n (oracle.c usize_zone); unused without lights
     d.light_zone = d.n_lights ? UINT64_MAX - (0ull - (uint64_t)d.n_lights) % (uint64_t)d.n_lights : 0;
     d.slt_mask = slt_mask(hs);
+    std::memset(d.lq_box, 0, sizeof(d.lq_box));
+    d.lq_boxes = lq_boxes(hs, d.lq_box);
     d.max_depth = 0;
     const DevBvh* all[6] = {&d.boxes, &d.ells, &d.tris, &d.lboxes, &d.lells, &d.ltris};
     for (int k = 0; k < 6; ++k) {

@@ -35,6 +35,7 @@ struct KParams {
 // light hits, lane steps, wave steps (64 x longest lane) — rt_stats order
 constexpr int kNStats = 10;
 constexpr int kStatsWords = 48;   // device counter words (rt_read_raw_stats)
+constexpr int kStatLqSkip = 10;  // raw word: last-bounce light queries the timed kernel skips
 constexpr int kPhaseWord0 = 16;   // RT_PHASES builds: region cycles + loop counts at words 16..33
 
 // Chunk count for a frame: a function of (W, H, spp) only, so the image does not

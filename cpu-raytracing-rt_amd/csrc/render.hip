@@ -1145,6 +1145,18 @@ RT_D V3 light_point(const DevScene& S, uint64_t A, uint64_t B, uint64_t C, Rng& 
     }
     return world;
 }
+// The last-bounce light query may be skipped: its origin q lies outside every
+// light's grown world box (DevScene::lq_boxes; zero when the scene does not qualify)
+RT_D bool lq_skippable(const DevScene& S, V3 q) {
+    const uint32_t n = uni_u32(S.lq_boxes);
+    if (n == 0) return false;
+    bool inside = false;
+    for (uint32_t i = 0; i < n; ++i) {
+        const double* b = S.lq_box[i];
+        inside = inside || (q.x >= b[0] && q.y >= b[1] && q.z >= b[2] && q.x <= b[3] && q.y <= b[4] && q.z <= b[5]);
+    }
+    return !inside && q.x == q.x && q.y == q.y && q.z == q.z;
+}
 RT_D double cosine_pdf(V3 n, V3 d) {  // ray_sampler.rs:78-83
     if (dot(n, d) <= 0.0) return 0.0;
     return dot(n, d) / kPi;
@@ -1264,7 +1276,16 @@ RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, P
             }
         }
         double lp = 0.0;
-        if (!empty) {
+        // On the path's last bounce only the pdf's NaN-ness is observable (below), and
+        // a query whose origin is outside every light's grown world box cannot give
+        // NaN (DevScene::lq_boxes): the timed kernel skips it.  The stats instance
+        // runs every query, so its counters stay the oracle's, and counts the skips.
+        bool query = !empty;
+        if (KM != kTris && last && query && lq_skippable(S, pos + dir * kEpsilon)) {  // box lights only
+            C.lqskip();
+            query = ST;
+        }
+        if (query) {
             const unsigned long long ph2 = PH_T();
             lp = light_pdf<ST, Stk, KM>(S, pos, dir, stk, C);
             PH_ADDW(kPhLightPdf, ph2);
@@ -1358,13 +1379,15 @@ RT_D bool segment(const DevScene& S, const KParams& P, const Scales& sc, PathSta
 template <bool ST>
 RT_D void wave_flush(const Cnt<ST>& C, unsigned long long* stats, uint32_t wave_iters) {
     if (!ST) return;
-    uint32_t v[8] = {C.c.paths, C.c.segments, C.c.aabb, C.c.tri, C.c.shape, C.c.shaded, C.c.lq, C.c.lhits};
+    uint32_t v[9] = {C.c.paths, C.c.segments, C.c.aabb, C.c.tri, C.c.shape, C.c.shaded, C.c.lq, C.c.lhits,
+                     C.c.lq_skip};
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < 9; ++k) {
+        const int w = k < 8 ? k : kStatLqSkip;
         unsigned long long x = v[k];
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
-        if ((threadIdx.x & 63) == 0 && x) atomicAdd(&stats[k], x);
+        if ((threadIdx.x & 63) == 0 && x) atomicAdd(&stats[w], x);
     }
     // lane utilisation: path steps summed over lanes vs 64 x the wave's loop iterations
     unsigned long long s = C.c.steps;

@@ -207,11 +207,13 @@ RT_D bool gen_bool(Rng& r, double p) {  // Bernoulli
 // ------------------------------------------------------------- counters ---
 struct Counters {
     uint32_t segments, aabb, tri, shape, shaded, lq, lhits, paths, steps;
+    uint32_t lq_skip;  // last-bounce light queries the timed kernel skips (DevScene::lq_boxes)
 };
 template <bool ON>
 struct Cnt {
     Counters c;
-    RT_D void zero() { if (ON) { c = Counters{0, 0, 0, 0, 0, 0, 0, 0, 0}; } }
+    RT_D void zero() { if (ON) { c = Counters{0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; } }
+    RT_D void lqskip() { if (ON) c.lq_skip++; }
     RT_D void segment() { if (ON) c.segments++; }
     RT_D void aabb(uint32_t n = 1) { if (ON) c.aabb += n; }
     RT_D void tri() { if (ON) c.tri++; }

@@ -152,7 +152,16 @@ struct DevScene {
     // records selected by the mask, in order: the light pdf of a diffuse bounce
     // then comes from the next segment's own box tests (same ray, same records).
     uint32_t slt_mask;
-    uint32_t _pad2;
+    // Last-bounce light query (render.hip segment_shade): nonzero only
+    // when every light is a box (at most kLqBoxes), each with a finite positive
+    // density.  Then a light query whose origin lies outside every box below (the
+    // lights' world boxes grown by a margin) has no crossing at t <= 0, so every
+    // term t^2 / |d.n| * density is positive or +inf and the pdf cannot be NaN; on
+    // the path's last bounce, where only the pdf's NaN-ness is observable, the
+    // timed kernel skips such queries.
+    uint32_t lq_boxes;
+    double lq_box[4][6];       // [light][min xyz, max xyz]
 };
+constexpr uint32_t kLqBoxes = 4;
 
 }  // namespace rt
