@@ -236,9 +236,11 @@ int rt_render_tiles_async(rt_scene* scene, const rt_render_params* params,
                           double* d_tile_rgb, void* hip_stream);
 
 /* Diagnostics: the scene's raw device counter words (n <= 48), accumulated by
-   RT_FLAG_STATS renders: words 0..9 are rt_stats' counters; builds compiled
+   RT_FLAG_STATS renders: words 0..9 are rt_stats' counters; word 10 counts the
+   last-bounce light queries the timed (no-stats) kernel skips because they cannot
+   be NaN (the stats render still runs them); builds compiled
    with -DRT_PHASES add wave cycles and loop counts per path-kernel region at
-   words 16..33 (tools/phases.py).  Not needed to render. */
+   words 16..46 (tools/phases.py).  Not needed to render. */
 int rt_read_raw_stats(rt_scene* scene, uint64_t* out, uint32_t n);
 
 /* Sample chunking of the work units: a pixel's spp samples are
