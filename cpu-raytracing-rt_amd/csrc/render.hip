@@ -305,9 +305,17 @@ RT_D void trav_enter(const DevBvh& B, Trav& T, uint32_t w) {
 // A compact triangle record (rt_layout.h kTriC: a, b, c as f32) in registers:
 // ba = b - a and ca = c - a rebuilt in f64, the host's bits (triangle_props).
 struct F3 { float x, y, z; };
+#ifdef RT_TRI_NT  // experiment: triangle records read with the non-temporal hint (streamed once, C5)
+typedef float v3f __attribute__((ext_vector_type(3)));
+RT_D F3 ld3(const float* p) {
+    const v3f v = __builtin_nontemporal_load((const v3f*)p);
+    return F3{v.x, v.y, v.z};
+}
+#else
+RT_D F3 ld3(const float* p) { return *(const F3*)p; }
+#endif
 RT_D TriRec load_tri_c(const float* __restrict__ p) {
-    const F3* q = (const F3*)p;
-    const F3 a = q[0], b = q[1], c = q[2];
+    const F3 a = ld3(p), b = ld3(p + 3), c = ld3(p + 6);
     asm volatile("" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(c.x), "v"(c.y), "v"(c.z));
     const V3 A = v3(a.x, a.y, a.z);
     return TriRec{A, v3(b.x, b.y, b.z) - A, v3(c.x, c.y, c.z) - A};
