@@ -334,7 +334,7 @@ RT_D TriRec widen_f9(const F9& r) {
 
 // Quad-shared node loads (RT_QUAD_NODE).  Scattered rays make every lane of a
 // 16-B load its own cache-line request: four per lane and node visit, the texture
-// addresser's work (TA busy 93% on C3).  Here the four lanes of a quad
+// addresser's work (TA busy ≈ 90% on C3).  Here the four lanes of a quad
 // load the four 16-B words of ONE lane's node per round (one line per quad, 16 per
 // wave-instruction instead of 64), for the quad's four lanes in turn, then a 4x4
 // transpose of 16-B words inside the quad (two DPP butterfly steps) gives each lane
