@@ -346,16 +346,21 @@ def main():
         dist.all_reduce(seg)
     frame_segments, frame_paths = int(seg[0].item()), int(seg[1].item())
 
+    # HIP events on the stream the kernels run on, per timed step: [render, gather,
+    # epilogue] boundaries (the gather and epilogue pair stay unrecorded in a PMC child)
     ev = []
 
+    def mark():
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(stream)
+        return e
+
     def step(timed):
-        if timed:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
+        marks = [mark()] if timed else None
         scene.render_tiles_async(params, rank, part, tiles.data_ptr(), sptr)
         if timed:
-            e1.record(stream)
-            ev.append((e0, e1))
+            marks.append(mark())
+            ev.append(marks)
         if part != world:  # PMC child: only the path kernel is of interest
             return
         if args.dist_backend == "nccl" or world == 1:
@@ -366,8 +371,12 @@ def main():
             if rank == 0:
                 gathered.copy_(g_host)
             src = gathered
+        if timed:
+            marks.append(mark())
         if rank == 0:
             rt.unpack_tiles_bytes_async(params, world, src.data_ptr(), image.data_ptr(), sptr)
+        if timed:
+            marks.append(mark())
 
     for _ in range(args.warmup):
         step(False)
@@ -385,7 +394,20 @@ def main():
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     elapsed = float(tt.item())
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    kern_ms = float(np.mean([m[0].elapsed_time(m[1]) for m in ev]))
+    # per-rank phases of the timed steps (mean ms): render kernel, the single gather
+    # (as this rank's stream sees it), the epilogue (rank 0) — so an N > 1 line
+    # separates rank imbalance from communication
+    phases = torch.tensor([kern_ms,
+                           float(np.mean([m[1].elapsed_time(m[2]) for m in ev])) if len(ev[0]) > 2 else 0.0,
+                           float(np.mean([m[2].elapsed_time(m[3]) for m in ev])) if len(ev[0]) > 3 else 0.0],
+                          dtype=torch.float64, device=dev)
+    if world > 1:
+        every = [torch.zeros_like(phases) for _ in range(world)]
+        dist.all_gather(every, phases)
+        per_rank = torch.stack(every).cpu().numpy()
+    else:
+        per_rank = phases.cpu().numpy()[None, :]
 
     if rank == 0 and part != world:  # PMC child: nothing to report
         return
@@ -448,6 +470,12 @@ def main():
             "paths_per_s": frame_paths * args.steps / elapsed,
             "tuning": scene.tuning(),
             "scene_build_s": build_s,
+            # HIP-event means over the timed steps, one entry per rank: the render kernel
+            # (incl. the chunk reduce), the gather as each rank's stream sees it, and rank
+            # 0's fused epilogue; max(render) / mean(render) is the render-side imbalance
+            "phases_ms": {"render": per_rank[:, 0].tolist(), "gather": per_rank[:, 1].tolist(),
+                          "epilogue": float(per_rank[0, 2]),
+                          "render_imbalance": float(per_rank[:, 0].max() / per_rank[:, 0].mean())},
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(desc, params, args.cpu_seconds)

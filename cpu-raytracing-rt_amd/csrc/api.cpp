@@ -172,11 +172,17 @@ int check_params(const rt_render_params* p) {
 
 // Sample chunking of a frame (render.h sample_chunks); a scene's tuning may
 // force the run length (rt_tuning.chunk_spp, tests and tuning experiments;
-// rt_scene_sample_chunks reports it, so checkers stay consistent).
+// rt_scene_sample_chunks reports it, so checkers stay consistent).  A forced run
+// length is raised, if need be, to keep the frame's rule's limits: at most
+// kMaxChunks runs, and the chunk partial sums within kPartBytes.
 void frame_chunks(const rt_render_params* p, uint32_t force_spp, uint32_t& chunks, uint32_t& chunk_spp) {
     sample_chunks(p->width, p->height, p->spp, chunks, chunk_spp);
     if (force_spp > 0) {
-        chunk_spp = std::min(force_spp, p->spp);
+        const uint64_t chunk_bytes =
+            (uint64_t)((p->width + 15) / 16) * ((p->height + 15) / 16) * 256 * 3 * sizeof(double);
+        const uint64_t max_chunks = std::max<uint64_t>(1, std::min<uint64_t>(kMaxChunks, kPartBytes / chunk_bytes));
+        const uint32_t floor_spp = (uint32_t)((p->spp + max_chunks - 1) / max_chunks);
+        chunk_spp = std::min(std::max(force_spp, floor_spp), p->spp);
         chunks = (p->spp + chunk_spp - 1) / chunk_spp;
     }
 }
@@ -277,13 +283,12 @@ bool path_resume(const rt_scene* s) {
 // 4-wave resumable kernel without a shape candidate carried across its loop
 // (C3 -6%), shape-only ones (the Cornell box) the fused kernel without triangle
 // traversal.  rt_tuning.kinds = 3 forces the general instances (tests, tuning).
-int path_kinds(const rt_scene* s) {
-    if (s->tune.kinds == 3) return 3;
-    const DevScene& d = s->dev;
+int scene_kinds(const DevScene& d) {
     const bool shapes = d.n_planes || d.boxes.n_prims || d.ells.n_prims || d.lboxes.n_prims || d.lells.n_prims;
     const bool tris = d.tris.n_prims || d.ltris.n_prims;
     return shapes == tris ? 3 : (shapes ? 1 : 2);
 }
+int path_kinds(const rt_scene* s) { return s->tune.kinds == 3 ? 3 : scene_kinds(s->dev); }
 
 // The triangle BVH's compact layout (rt_layout.h DevNodeC, half the bytes per
 // node visit and triangle test, the same numbers): used by the triangle-only
@@ -297,10 +302,15 @@ bool path_compact(const rt_scene* s) {
 // Suspend threshold of the resumable traversal (render.h kSuspendCached /
 // kSuspendStreamed): by whether the triangle BVH and its hot records fit the
 // Infinity Cache.  rt_tuning.suspend_lanes forces one (tuning).
-bool bvh_streamed(const rt_scene* s) {  // the triangle BVH and its hot records exceed the Infinity Cache
-    const uint64_t bytes = s->info.bvh_nodes[2] * sizeof(DevNode) + s->info.n_triangles * sizeof(DevTri);
-    return bytes > kCacheBytes;
+// The triangle BVH and its hot records exceed the Infinity Cache, sized by the
+// layout the kernel reads (path_compact: 64-B nodes and 36-B records, else 128 B
+// and 80 B).
+uint64_t bvh_hot_bytes(const rt_scene* s) {
+    const bool cmp = path_compact(s);
+    return s->info.bvh_nodes[2] * (cmp ? sizeof(DevNodeC) : sizeof(DevNode)) +
+           s->info.n_triangles * (cmp ? kTriC * sizeof(float) : sizeof(DevTri));
 }
+bool bvh_streamed(const rt_scene* s) { return bvh_hot_bytes(s) > kCacheBytes; }
 uint32_t path_suspend(const rt_scene* s) {
     if (s->tune.suspend_lanes) return s->tune.suspend_lanes;
     return bvh_streamed(s) ? kSuspendStreamed : kSuspendCached;
@@ -368,12 +378,17 @@ uint32_t slt_mask(const HostScene& hs) {
     return j == L.shapes.size() ? mask : 0;
 }
 
-// DevScene::lq_boxes / lq_box: the light boxes' world-space bounds (the eight
-// corners pos + rotate(rot, +-half sizes); model_ray maps world to model space by
-// the conjugate, so model to world is rot itself), grown by a margin of 1e-6 of
-// the coordinates' magnitude (+1e-100) that dwarfs the rounding of the rotation and
-// of the query's slab arithmetic.  Zero (no skipping) unless every light is a box,
-// there are at most kLqBoxes, and every box and density is finite and positive.
+// DevScene::lq_boxes / lq_box: the light boxes' world-space bounds, grown by a
+// margin of 1e-6 of the coordinates' magnitude (+1e-100) that dwarfs the rounding
+// of the model-space map and of the query's slab arithmetic.  model_ray maps a
+// world point p to M (p - pos) with M = x -> rotate(conj(rot), x), cgmath's
+// rotate_vector: for a quaternion of norm n = |rot|^2 that is n R^T + (1 - n) I,
+// a rotation only when n == 1 (the parser, like the reference, does not
+// normalise ROTATION).  The box surface is therefore pos + M^-1 (+-half sizes):
+// the eight corners come through the inverse of M, built from rotate() on the
+// basis vectors and inverted here.  Zero (no skipping) unless every light is a
+// box, there are at most kLqBoxes, every box and density is finite and positive,
+// and M is well conditioned (n within 10% of 1, the inverse checked).
 uint32_t lq_boxes(const HostScene& hs, double (*out)[6]) {
     const auto& L = hs.bvh[3].shapes;
     if (L.empty() || L.size() > kLqBoxes || !hs.bvh[4].shapes.empty() || !hs.bvh[5].tris.empty()) return 0;
@@ -382,11 +397,35 @@ uint32_t lq_boxes(const HostScene& hs, double (*out)[6]) {
         const double pb = b.aux[0];
         if (!(pb > 0.0) || !std::isfinite(pb)) return 0;
         const Quat q = load_quat(b.rot);
+        const double n = q.s * q.s + dot(q.v, q.v);
+        if (!(std::fabs(n - 1.0) <= 0.1)) return 0;
+        const Quat c = conjugate(q);
+        double M[3][3], Mi[3][3];
+        for (int k = 0; k < 3; ++k) {  // column k = M e_k
+            const V3 col = rotate(c, v3(k == 0, k == 1, k == 2));
+            M[0][k] = col.x; M[1][k] = col.y; M[2][k] = col.z;
+        }
+        const double det = M[0][0] * (M[1][1] * M[2][2] - M[1][2] * M[2][1]) -
+                           M[0][1] * (M[1][0] * M[2][2] - M[1][2] * M[2][0]) +
+                           M[0][2] * (M[1][0] * M[2][1] - M[1][1] * M[2][0]);
+        if (!(std::fabs(det) > 0.5)) return 0;
+        for (int r = 0; r < 3; ++r)
+            for (int k = 0; k < 3; ++k) {  // adjugate / det
+                const int r1 = (k + 1) % 3, r2 = (k + 2) % 3, c1 = (r + 1) % 3, c2 = (r + 2) % 3;
+                Mi[r][k] = (M[r1][c1] * M[r2][c2] - M[r1][c2] * M[r2][c1]) / det;
+            }
+        for (int r = 0; r < 3; ++r)  // M Mi == I to 1e-12
+            for (int k = 0; k < 3; ++k) {
+                const double e = M[r][0] * Mi[0][k] + M[r][1] * Mi[1][k] + M[r][2] * Mi[2][k];
+                if (!(std::fabs(e - (r == k ? 1.0 : 0.0)) <= 1e-12)) return 0;
+            }
         V3 lo = v3(INFINITY, INFINITY, INFINITY), hi = v3(-INFINITY, -INFINITY, -INFINITY);
-        for (int c = 0; c < 8; ++c) {
-            const V3 h = v3((c & 1) ? b.shape[0] : -b.shape[0], (c & 2) ? b.shape[1] : -b.shape[1],
-                            (c & 4) ? b.shape[2] : -b.shape[2]);
-            const V3 p = load3(b.pos) + rotate(q, h);
+        for (int k = 0; k < 8; ++k) {
+            const double h[3] = {(k & 1) ? b.shape[0] : -b.shape[0], (k & 2) ? b.shape[1] : -b.shape[1],
+                                 (k & 4) ? b.shape[2] : -b.shape[2]};
+            const V3 p = load3(b.pos) + v3(Mi[0][0] * h[0] + Mi[0][1] * h[1] + Mi[0][2] * h[2],
+                                           Mi[1][0] * h[0] + Mi[1][1] * h[1] + Mi[1][2] * h[2],
+                                           Mi[2][0] * h[0] + Mi[2][1] * h[1] + Mi[2][2] * h[2]);
             lo = v3(std::min(lo.x, p.x), std::min(lo.y, p.y), std::min(lo.z, p.z));
             hi = v3(std::max(hi.x, p.x), std::max(hi.y, p.y), std::max(hi.z, p.z));
         }
@@ -509,7 +548,7 @@ int scene_upload(const HostScene& hs, rt_scene** out) {
     s->info.n_light_ellipsoids = d.lells.n_prims;
     s->info.n_light_triangles = d.ltris.n_prims;
     s->info.shared_light_mask = d.slt_mask;
-    s->info.layout_flags = d.tris.cnodes ? RT_LAYOUT_COMPACT_TRIS : 0u;
+    s->info.layout_flags = (d.tris.cnodes ? RT_LAYOUT_COMPACT_TRIS : 0u) | (d.lq_boxes ? RT_LAYOUT_LQ_SKIP : 0u);
     s->info.build_ms = hs.build_ms;
     s->info.upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     *out = owner.release();
@@ -557,9 +596,14 @@ int rt_scene_set_tuning(rt_scene* s, const rt_tuning* t) {
     if (!t) { s->tune = rt_tuning{0, -1, 0, 0, 0, 0, -1, 0}; return RT_OK; }
     if (t->waves != 0 && t->waves != 3 && t->waves != 4) return set_error(RT_ERR_INVALID, "waves must be 0, 3 or 4");
     if (t->resume < -1 || t->resume > 1) return set_error(RT_ERR_INVALID, "resume must be -1, 0 or 1");
-    if (t->kinds != 0 && t->kinds != 3) return set_error(RT_ERR_INVALID, "kinds must be 0 or 3");
+    if (t->kinds > 3) return set_error(RT_ERR_INVALID, "kinds must be 0..3");
+    // 1 / 2 (what rt_scene_get_tuning reports for a one-kind scene): only the scene's own kinds
+    if ((t->kinds == 1 || t->kinds == 2) && (int)t->kinds != scene_kinds(s->dev))
+        return set_error(RT_ERR_INVALID, "kinds 1/2 must be the scene's own primitive kinds (0 or 3 otherwise)");
     if (t->suspend_lanes > 64 || t->leaf_lanes > 64) return set_error(RT_ERR_INVALID, "lane counts must be <= 64");
     if (t->compact < -1 || t->compact > 1) return set_error(RT_ERR_INVALID, "compact must be -1, 0 or 1");
+    if (t->compact == 1 && !s->dev.tris.cnodes)
+        return set_error(RT_ERR_UNSUPPORTED, "compact = 1: the scene has no compact triangle layout");
     s->tune = *t;
     return RT_OK;
 }

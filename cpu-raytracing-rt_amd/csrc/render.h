@@ -36,6 +36,9 @@ struct KParams {
 constexpr int kNStats = 10;
 constexpr int kStatsWords = 48;   // device counter words (rt_read_raw_stats)
 constexpr int kStatLqSkip = 10;  // raw word: last-bounce light queries the timed kernel skips
+// raw words 11..13: inner-node visits of closest-hit traversals whose child boxes
+// were hit by none / one / both of the two slab tests (stats instances only)
+constexpr int kStatKids0 = 11;
 constexpr int kPhaseWord0 = 16;   // RT_PHASES builds: region cycles + loop counts at words 16..33
 
 // Chunk count for a frame: a function of (W, H, spp) only, so the image does not

@@ -30,10 +30,7 @@ namespace rt {
 
 constexpr int kBlock = 256;
 constexpr int kShort = kMaxBvhDepthShort;
-#ifndef RT_LEAF_BATCH
-#define RT_LEAF_BATCH 16  // lanes waiting at leaves before the wave tests primitives (bvh_closest)
-#endif
-constexpr int kLeafBatch = RT_LEAF_BATCH;
+constexpr int kLeafBatch = 16;  // lanes waiting at leaves before the wave tests primitives (bvh_closest)
 
 // ---------------------------------------------------------------- stack ---
 // LDS short stack laid out per wave: [wave][slot][lane], so consecutive lanes
@@ -219,50 +216,19 @@ RT_D bool slab(const double* mn, const double* mx, V3 o, V3 d, const Rcp3& rc, b
 // loads.  The asm pins the right box's registers before the left slab test is
 // computed, so the compiler cannot sink the right box's loads behind that test:
 // one memory round trip per node visit instead of two (C3 -3.3%, C5 -6.3% at
-// reduced spp, profiles/r02/variants/variants_preload_*.log).  RT_NODE_LAZY:
-// the former per-box loads (ablation).
+// reduced spp, profiles/r02/variants/variants_preload_*.log).
 struct NodeBoxes { V3 lmn, lmx, rmn, rmx; };
 RT_D NodeBoxes node_boxes(const DevNode& n) {
-#ifndef RT_NODE_LAZY
     const double2* nw = (const double2*)&n;
     const double2 w0 = nw[0], w1 = nw[1], w2 = nw[2], w3 = nw[3], w4 = nw[4], w5 = nw[5];
     asm volatile("" ::"v"(w3.x), "v"(w3.y), "v"(w4.x), "v"(w4.y), "v"(w5.x), "v"(w5.y));
     return NodeBoxes{v3(w0.x, w0.y, w1.x), v3(w1.y, w2.x, w2.y), v3(w3.x, w3.y, w4.x), v3(w4.y, w5.x, w5.y)};
-#else
-    return NodeBoxes{load3(n.lmin), load3(n.lmax), load3(n.rmin), load3(n.rmax)};
-#endif
-}
-// Experiment (RT_SLAB_SIGNED; measured neutral on C3/C5, so the min/max form is the
-// default): the unguarded slab test of a compact (f32) box with the near and far
-// planes picked by the direction's signs before widening.  For a fast ray d has no zero component, and the quotient
-// RN(RN(v - o) / d) is monotone in v — non-decreasing for d > 0, non-increasing for
-// d < 0 — so min(q(lo), q(hi)) is q(lo) when d > 0 and q(hi) when d < 0 (equal
-// values when they tie): the same tn, tf and t as aabb_hit_fast, with one 32-bit
-// select per plane instead of an f64 min and max per axis.
-RT_D bool aabb_hit_fast_c(float lx, float ly, float lz, float hx, float hy, float hz, V3 o, const Rcp3& rc, V3 d,
-                          double& t) {
-    const bool nx = __double2hiint(d.x) < 0, ny = __double2hiint(d.y) < 0, nz = __double2hiint(d.z) < 0;
-    const double ax = dev_quot((double)(nx ? hx : lx) - o.x, d.x, rc.r.x);
-    const double bx = dev_quot((double)(nx ? lx : hx) - o.x, d.x, rc.r.x);
-    const double ay = dev_quot((double)(ny ? hy : ly) - o.y, d.y, rc.r.y);
-    const double by = dev_quot((double)(ny ? ly : hy) - o.y, d.y, rc.r.y);
-    const double az = dev_quot((double)(nz ? hz : lz) - o.z, d.z, rc.r.z);
-    const double bz = dev_quot((double)(nz ? lz : hz) - o.z, d.z, rc.r.z);
-    const double tn = __builtin_fmax(__builtin_fmax(ax, ay), az);
-    const double tf = __builtin_fmin(__builtin_fmin(bx, by), bz);
-    t = __builtin_fmax(tn, 0.0);
-    return tn <= tf && 0.0 <= tf;
 }
 template <int SLAB>
 RT_D bool slab_c(float lx, float ly, float lz, float hx, float hy, float hz, V3 o, V3 d, const Rcp3& rc, bool fast,
                  double& t) {
-#ifdef RT_SLAB_SIGNED
-    if (SLAB == 1 || (SLAB == 2 && fast)) return aabb_hit_fast_c(lx, ly, lz, hx, hy, hz, o, rc, d, t);
-    return aabb_hit<false>(v3(lx, ly, lz), v3(hx, hy, hz), o, d, rc, t);
-#else
     if (SLAB == 1 || (SLAB == 2 && fast)) return aabb_hit<true>(v3(lx, ly, lz), v3(hx, hy, hz), o, d, rc, t);
     return aabb_hit<false>(v3(lx, ly, lz), v3(hx, hy, hz), o, d, rc, t);
-#endif
 }
 template <int SLAB>
 RT_D bool slab_v(V3 mn, V3 mx, V3 o, V3 d, const Rcp3& rc, bool fast, double& t) {  // boxes already loaded
@@ -305,15 +271,7 @@ RT_D void trav_enter(const DevBvh& B, Trav& T, uint32_t w) {
 // A compact triangle record (rt_layout.h kTriC: a, b, c as f32) in registers:
 // ba = b - a and ca = c - a rebuilt in f64, the host's bits (triangle_props).
 struct F3 { float x, y, z; };
-#ifdef RT_TRI_NT  // experiment: triangle records read with the non-temporal hint (streamed once, C5)
-typedef float v3f __attribute__((ext_vector_type(3)));
-RT_D F3 ld3(const float* p) {
-    const v3f v = __builtin_nontemporal_load((const v3f*)p);
-    return F3{v.x, v.y, v.z};
-}
-#else
 RT_D F3 ld3(const float* p) { return *(const F3*)p; }
-#endif
 RT_D TriRec load_tri_c(const float* __restrict__ p) {
     const F3 a = ld3(p), b = ld3(p + 3), c = ld3(p + 6);
     asm volatile("" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(c.x), "v"(c.y), "v"(c.z));
@@ -321,69 +279,6 @@ RT_D TriRec load_tri_c(const float* __restrict__ p) {
     return TriRec{A, v3(b.x, b.y, b.z) - A, v3(c.x, c.y, c.z) - A};
 }
 
-// the same record as its nine floats (a prefetch that holds 9 VGPRs, widened later)
-struct F9 { F3 a, b, c; };
-RT_D F9 load_f9(const float* __restrict__ p) {
-    const F3* q = (const F3*)p;
-    return F9{q[0], q[1], q[2]};
-}
-RT_D TriRec widen_f9(const F9& r) {
-    const V3 A = v3(r.a.x, r.a.y, r.a.z);
-    return TriRec{A, v3(r.b.x, r.b.y, r.b.z) - A, v3(r.c.x, r.c.y, r.c.z) - A};
-}
-
-// Quad-shared node loads (RT_QUAD_NODE).  Scattered rays make every lane of a
-// 16-B load its own cache-line request: four per lane and node visit, the texture
-// addresser's work (TA busy ≈ 90% on C3).  Here the four lanes of a quad
-// load the four 16-B words of ONE lane's node per round (one line per quad, 16 per
-// wave-instruction instead of 64), for the quad's four lanes in turn, then a 4x4
-// transpose of 16-B words inside the quad (two DPP butterfly steps) gives each lane
-// its own node's words.  The same bytes reach the same lanes.
-#ifdef RT_QUAD_NODE
-constexpr bool kQuadNode = true;
-template <int CTRL>
-RT_D uint32_t dppq(uint32_t v) { return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xF, 0xF, false); }
-template <int CTRL>
-RT_D uint4 dppq4(uint4 v) { return make_uint4(dppq<CTRL>(v.x), dppq<CTRL>(v.y), dppq<CTRL>(v.z), dppq<CTRL>(v.w)); }
-RT_D uint4 sel4(bool c, uint4 a, uint4 b) { return c ? a : b; }
-RT_D float4 u4f(uint4 v) {
-    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
-}
-RT_D void quad_node_load(const DevNodeC* __restrict__ nodes, uint32_t node, bool inner, uint4& y0, uint4& y1,
-                         uint4& y2, uint4& y3) {
-    const uint32_t lane = stack_lane();
-    const uint32_t qi = lane & 3u;
-    const uint64_t im = __ballot(inner) >> (lane & ~3u);  // bit r: the quad's lane r is at an inner node
-    const uint4* base = (const uint4*)nodes;
-    uint4 x[4];
-    const uint32_t n0 = dppq<0x00>(node), n1 = dppq<0x55>(node), n2 = dppq<0xAA>(node), n3 = dppq<0xFF>(node);
-    // round r: word qi of the node of the quad's lane r (quad_perm broadcast of its index)
-    x[0] = (im & 1u) ? base[(size_t)n0 * 4 + qi] : make_uint4(0, 0, 0, 0);
-    x[1] = (im & 2u) ? base[(size_t)n1 * 4 + qi] : make_uint4(0, 0, 0, 0);
-    x[2] = (im & 4u) ? base[(size_t)n2 * 4 + qi] : make_uint4(0, 0, 0, 0);
-    x[3] = (im & 8u) ? base[(size_t)n3 * 4 + qi] : make_uint4(0, 0, 0, 0);
-    // lane i slot r = word i of node(r) -> word r of node(i): swap with lane i ^ 1 the
-    // slots whose bit 0 differs from i's, then with lane i ^ 2 those whose bit 1 does
-    const bool odd = qi & 1u, hi = qi & 2u;
-    {
-        const uint4 r0 = dppq4<0xB1>(sel4(odd, x[0], x[1])), r1 = dppq4<0xB1>(sel4(odd, x[2], x[3]));
-        if (odd) { x[0] = r0; x[2] = r1; } else { x[1] = r0; x[3] = r1; }
-    }
-    {
-        const uint4 r0 = dppq4<0x4E>(sel4(hi, x[0], x[2])), r1 = dppq4<0x4E>(sel4(hi, x[1], x[3]));
-        if (hi) { x[0] = r0; x[1] = r1; } else { x[2] = r0; x[3] = r1; }
-    }
-    y0 = x[0]; y1 = x[1]; y2 = x[2]; y3 = x[3];
-}
-#else
-constexpr bool kQuadNode = false;
-#endif
-
-#ifdef RT_RECOMPUTE_UV  // experiment: the compact kernel re-tests the winner for (u, v) instead of carrying them
-constexpr bool kRecomputeUV = true;
-#else
-constexpr bool kRecomputeUV = false;
-#endif
 // CMP: the triangle BVH's compact layout (DevBvh::cnodes / ctris, KIND 3 only):
 // the same boxes and vertices as exact f32 copies, widened to f64 before the
 // same arithmetic — every lane's visits, tests and results are the f64 form's.
@@ -397,98 +292,70 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
     bool next = false;  // this lane finished its current node and pops
     if (do_leaves) {
         if (T.live && T.cnt != 0) {
-#ifndef RT_LEAF_SEQ  // ablation build: one record load per loop trip
             if constexpr (KIND == 3) {
-                // Software-pipelined leaf: the next triangle's record loads while this one
-                // is tested (C3 -0.8%, C5 -1.0% at reduced spp, variants_leafpipe_*.log).
                 const uint32_t end = T.start + T.cnt;
-#ifndef RT_LEAF_PIPE_CMP  // ablation build: the compact records software-pipelined too
                 if constexpr (CMP) {
-                    // Compact records are loaded when tested: the pipelined form holds the
+                    // Compact records are loaded when tested: a pipelined form holds the
                     // next record widened (18 VGPRs) through the test, which the 4-wave
                     // kernel pays in spills (a traversal-only kernel needs 105 VGPRs with it,
                     // 84 without): C3 -0.9%, C5 -1.9% at reduced spp
-                    // (profiles/r03/variants/variants_leafpipe_C*.log).  RT_LEAF_RAWPIPE:
-                    // prefetch the next record as its nine floats (C3 -0.4%, C5 -2.1%).
-#ifdef RT_LEAF_RAWPIPE
-                    F9 nraw = load_f9(B.ctris + (size_t)T.start * kTriC);
-#endif
+                    // (profiles/r03/variants/variants_leafpipe_C*.log).
                     for (uint32_t i = T.start; i < end; ++i) {
                         PH_COUNT(kPhLeafWave, kPhLeafLane);
-#ifdef RT_LEAF_RAWPIPE
-                        const F9 craw = nraw;
-                        if (i + 1 < end) nraw = load_f9(B.ctris + (size_t)(i + 1) * kTriC);
-                        const TriRec cur = widen_f9(craw);
-#else
                         const TriRec cur = load_tri_c(B.ctris + (size_t)i * kTriC);
-#endif
                         double t, u = 0.0, v = 0.0;
                         C.tri();
                         const bool h = tri_uvt_r(cur, o, d, u, v, t);
                         if (h && (!T.valid || t < T.best)) {  // update_best_intersection (bvh.rs:213-222)
                             T.valid = true; T.best = t; T.prim = i; T.aux = 0;
-                            if (!kRecomputeUV) { T.bu = u; T.bv = v; }
+                            T.bu = u; T.bv = v;
                         }
                     }
-                } else
-#endif
-                {
-                TriRec cur = CMP ? load_tri_c(B.ctris + (size_t)T.start * kTriC) : load_tri(B.tris[T.start]);
-                for (uint32_t i = T.start; i < end; ++i) {
-                    PH_COUNT(kPhLeafWave, kPhLeafLane);
-                    TriRec nxt = cur;
-                    if (i + 1 < end) nxt = CMP ? load_tri_c(B.ctris + (size_t)(i + 1) * kTriC) : load_tri(B.tris[i + 1]);
-                    double t, u = 0.0, v = 0.0;
-                    C.tri();
-                    const bool h = tri_uvt_r(cur, o, d, u, v, t);
-                    if (h && (!T.valid || t < T.best)) {  // update_best_intersection (bvh.rs:213-222)
-                        T.valid = true; T.best = t; T.prim = i; T.aux = 0;
-                        if (!(CMP && kRecomputeUV)) { T.bu = u; T.bv = v; }
+                } else {
+                    // Software-pipelined leaf: the next triangle's record loads while this one
+                    // is tested (C3 -0.8%, C5 -1.0% at reduced spp, variants_leafpipe_*.log).
+                    TriRec cur = load_tri(B.tris[T.start]);
+                    for (uint32_t i = T.start; i < end; ++i) {
+                        PH_COUNT(kPhLeafWave, kPhLeafLane);
+                        TriRec nxt = cur;
+                        if (i + 1 < end) nxt = load_tri(B.tris[i + 1]);
+                        double t, u = 0.0, v = 0.0;
+                        C.tri();
+                        const bool h = tri_uvt_r(cur, o, d, u, v, t);
+                        if (h && (!T.valid || t < T.best)) {  // update_best_intersection (bvh.rs:213-222)
+                            T.valid = true; T.best = t; T.prim = i; T.aux = 0;
+                            T.bu = u; T.bv = v;
+                        }
+                        cur = nxt;
                     }
-                    cur = nxt;
                 }
-                }
-            } else
-#endif
-            for (uint32_t i = T.start; i < T.start + T.cnt; ++i) {
-                PH_COUNT(kPhLeafWave, kPhLeafLane);
-                double t, u = 0.0, v = 0.0;
-                uint32_t aux = 0;
-                bool h;
-                if (KIND == 3) { C.tri(); h = tri_uvt(B.tris[i], o, d, u, v, t); }
-                else { C.shape(); h = shape_closest<KIND>(B.shapes[i], o, d, rc, fast, t, aux); }
-                if (h && (!T.valid || t < T.best)) {  // update_best_intersection (bvh.rs:213-222)
-                    T.valid = true; T.best = t; T.bu = u; T.bv = v; T.prim = i; T.aux = aux;
+            } else {
+                for (uint32_t i = T.start; i < T.start + T.cnt; ++i) {
+                    PH_COUNT(kPhLeafWave, kPhLeafLane);
+                    double t, u = 0.0, v = 0.0;
+                    uint32_t aux = 0;
+                    C.shape();
+                    const bool h = shape_closest<KIND>(B.shapes[i], o, d, rc, fast, t, aux);
+                    if (h && (!T.valid || t < T.best)) {  // update_best_intersection (bvh.rs:213-222)
+                        T.valid = true; T.best = t; T.bu = u; T.bv = v; T.prim = i; T.aux = aux;
+                    }
                 }
             }
             next = true;
         }
-    } else if (CMP && (kQuadNode || (T.live && T.cnt == 0))) {  // internal node, compact layout (64 B)
-#ifdef RT_QUAD_NODE
-        // Quad-shared node loads: the whole wave is here (do_leaves is uniform); see
-        // quad_node_load.  Lanes not at an inner node take part in their quad's loads.
-        const bool inner = T.live && T.cnt == 0;
-        uint4 q0, q1, q2, q3;
-        quad_node_load(B.cnodes, T.node, inner, q0, q1, q2, q3);
-        if (inner) {
-        const float4 w0 = u4f(q0), w1 = u4f(q1), w2 = u4f(q2);
-        const uint2 k = make_uint2(q3.x, q3.y);
-#else
-        {
+    } else if (CMP && T.live && T.cnt == 0) {  // internal node, compact layout (64 B)
+        // both children's f32 boxes and their two child words (56 of the 64 B: a leaf's
+        // own range is read by trav_enter)
         const float4* nw = (const float4*)(B.cnodes + T.node);
         const float4 w0 = nw[0], w1 = nw[1], w2 = nw[2];
-#ifndef RT_NODE_K4  // the two child words only (56 of the 64 B: a leaf's own range is read by trav_enter)
         const uint2 k = ((const uint2*)nw)[6];
-#else  // ablation build: the whole fourth 16-B word
-        const uint4 k = ((const uint4*)nw)[3];
-#endif
         asm volatile("" ::"v"(w1.z), "v"(w1.w), "v"(w2.x), "v"(w2.y), "v"(w2.z), "v"(w2.w));  // see node_boxes
-#endif
         PH_COUNT(kPhInnerWave, kPhInnerLane);
         double lt = 0.0, rt2 = 0.0;
         C.aabb(2);
         const bool lh = slab_c<SLAB>(w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, o, d, rc, fast, lt);
         const bool rh = slab_c<SLAB>(w1.z, w1.w, w2.x, w2.y, w2.z, w2.w, o, d, rc, fast, rt2);
+        C.kids(lh, rh);
         const double bt = T.best;  // +inf when no hit yet
         const double li = lh ? (lt < bt ? lt : bt) : bt;
         const double ri = rh ? (rt2 < bt ? rt2 : bt) : bt;
@@ -500,7 +367,6 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
             } else go_left = true;
         } else if (!(ri < bt)) next = true;
         if (!next) trav_enter<true>(B, T, go_left ? k.x : k.y);
-        }
     } else if (!CMP && T.live && T.cnt == 0) {  // internal node (count 0 <=> children)
         PH_COUNT(kPhInnerWave, kPhInnerLane);
         const DevNode& n = B.nodes[T.node];
@@ -509,11 +375,9 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
         double lt = 0.0, rt2 = 0.0;
         C.aabb(2);
         const NodeBoxes nb = node_boxes(n);
-#ifdef RT_PIN_META
-        asm volatile("" ::"v"(links.x), "v"(links.y), "v"(kids.x), "v"(kids.y), "v"(kids.z), "v"(kids.w));
-#endif
         const bool lh = slab_v<SLAB>(nb.lmn, nb.lmx, o, d, rc, fast, lt);
         const bool rh = slab_v<SLAB>(nb.rmn, nb.rmx, o, d, rc, fast, rt2);
+        C.kids(lh, rh);
         const double bt = T.best;  // +inf when no hit yet
         const double li = lh ? (lt < bt ? lt : bt) : bt;
         const double ri = rh ? (rt2 < bt ? rt2 : bt) : bt;
@@ -575,15 +439,10 @@ RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stk& S, Cnt<S
     bool valid = false;
     double best = INFINITY;
     if (B.depth == 1) {  // the root is the only leaf (bvh.rs:77, <= 4 primitives): [0, n_prims) in order
-#ifndef RT_NO_UNI  // uniform index: the records come through the scalar cache
+        // uniform index: the records come through the scalar cache
         const uint32_t np = uni_u32(B.n_prims);
         const RT_CAS DevTri* tris = uni(B.tris);
         const RT_CAS DevShape* shapes = uni(B.shapes);
-#else
-        const uint32_t np = B.n_prims;
-        const DevTri* tris = B.tris;
-        const DevShape* shapes = B.shapes;
-#endif
         auto test = [&](uint32_t i) {
             double t, u = 0.0, v = 0.0;
             uint32_t aux = 0;
@@ -640,6 +499,7 @@ RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stk& S, Cnt<S
             C.aabb(2);
             bool lh = aabb_hit<FAST>(load3(n.lmin), load3(n.lmax), o, d, rc, lt);
             bool rh = aabb_hit<FAST>(load3(n.rmin), load3(n.rmax), o, d, rc, rt2);
+            C.kids(lh, rh);
             const double bt = best;  // +inf when no hit yet
             const double li = lh ? (lt < bt ? lt : bt) : bt;
             const double ri = rh ? (rt2 < bt ? rt2 : bt) : bt;
@@ -848,13 +708,8 @@ RT_D void shapes_closest(const DevScene& S, V3 o, V3 d, const Rcp3& rc, bool rfa
                          Cand& best, bool pend = false, double* impact = nullptr) {
     best.valid = false; best.t = 0.0; best.u = best.v = 0.0; best.prim = 0; best.aux = 0; best.kind = 0;
     unsigned long long ph = PH_T();
-#ifndef RT_NO_UNI  // ablation build: per-lane flat loads of the plane records
     const uint32_t np = uni_u32(S.n_planes);
     const RT_CAS DevShape* planes = uni(S.planes);
-#else
-    const uint32_t np = S.n_planes;
-    const DevShape* planes = S.planes;
-#endif
     // the first 8 planes unrolled (a uniform early exit): their records' scalar
     // loads issue together instead of one loop trip at a time (C2 -1.9%)
 #pragma unroll
@@ -953,11 +808,7 @@ RT_D double prob_ell(V3 r, V3 ng) {
 template <int KIND, bool ST, bool UNI = false>
 RT_D void leaf_all(const DevBvh& B, uint32_t start, uint32_t cnt, V3 o, V3 d, const Rcp3& rc, bool rfast,
                    Cnt<ST>& C, double& impact, uint32_t& nhits) {
-#ifdef RT_NO_UNI
-    constexpr bool kUni = false;
-#else
     constexpr bool kUni = UNI;
-#endif
     if (kUni) cnt = uni_u32(cnt);
     for (uint32_t i = start; i < start + cnt; ++i) {
         if (KIND == 3) {
@@ -1238,12 +1089,8 @@ RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, P
     const V3 col = load3(m.color);
     ps.L = ps.L + mul(ps.T, load3(m.emission));
     // The last segment shades like every other: its direction and pdf decide
-    // whether raytrace_impl's last level is NaN (below).  RT_LASTSEG_SHORTCUT is the
-    // round-2 form that stopped after the emission (C2 -2.6% at 64 spp, but it
-    // misses that NaN, so it is an ablation build only).
-#ifdef RT_LASTSEG_SHORTCUT
-    if (!ST && last) return false;
-#endif
+    // whether raytrace_impl's last level is NaN (below).  (Stopping after the
+    // emission, round 2, was 2.6% faster on C2 but misses that NaN.)
     rng_align(rng);   // shading draws start on a block boundary (oracle.c rng_align)
     rng_top_up(rng);  // every hit lane here: a coherent refill point
     const V3 o = ps.o, d = ps.d;
@@ -1355,10 +1202,6 @@ RT_D bool segment_end(const DevScene& S, const KParams& P, const Scales& sc, Pat
         q.best.valid = false; q.best.t = 0.0; q.best.u = q.best.v = 0.0; q.best.prim = 0; q.best.aux = 0;
         q.best.kind = 0;
     }
-    if (CMP && kRecomputeUV && q.T.valid) {  // the winner's (u, v): the same test, the same bits
-        double t;
-        (void)tri_uvt_r(load_tri_c(S.tris.ctris + (size_t)q.T.prim * kTriC), ps.o, ps.d, q.T.bu, q.T.bv, t);
-    }
     take_tri(q.best, q.T.valid, q.T.best, q.T.bu, q.T.bv, q.T.prim);
     const bool hit = intersect_tail<ST, KM>(S, q.best, ps.o, ps.d, C, h, mat, gid);
     return segment_shade<ST, Stk, false, KM>(S, P, sc, ps, rng, stk, C, hit, h, mat, gid, hit_gid, false, last);
@@ -1387,11 +1230,11 @@ RT_D bool segment(const DevScene& S, const KParams& P, const Scales& sc, PathSta
 template <bool ST>
 RT_D void wave_flush(const Cnt<ST>& C, unsigned long long* stats, uint32_t wave_iters) {
     if (!ST) return;
-    uint32_t v[9] = {C.c.paths, C.c.segments, C.c.aabb, C.c.tri, C.c.shape, C.c.shaded, C.c.lq, C.c.lhits,
-                     C.c.lq_skip};
+    uint32_t v[12] = {C.c.paths, C.c.segments, C.c.aabb, C.c.tri, C.c.shape, C.c.shaded, C.c.lq, C.c.lhits,
+                      C.c.lq_skip, C.c.kids[0], C.c.kids[1], C.c.kids[2]};
 #pragma unroll
-    for (int k = 0; k < 9; ++k) {
-        const int w = k < 8 ? k : kStatLqSkip;
+    for (int k = 0; k < 12; ++k) {
+        const int w = k < 8 ? k : kStatLqSkip + (k - 8);
         unsigned long long x = v[k];
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
@@ -1450,14 +1293,9 @@ constexpr uint32_t kCamSlots = 128;  // precomputed camera rays per wave (two sa
 // flat loads, each a full vector-memory round trip.
 template <class T>
 RT_D const T* opaque(const T* p) {
-#ifndef RT_FLAT_SCENE  // ablation build: the generic pointer
     const RT_CAS T* q = (const RT_CAS T*)p;
     asm volatile("" : "+s"(q));
     return (const T*)q;
-#else
-    asm volatile("" : "+s"(p));
-    return p;
-#endif
 }
 
 // A wave-tile (tile slot, sample chunk, 8x8 quadrant) in frame coordinates.
@@ -1494,20 +1332,10 @@ RT_D uint32_t unit_of_row(const uint32_t* uq, uint32_t uq_back, uint32_t row) {
     return i % kUQ;
 }
 
-// waves per SIMD the 4-wave resumable kernel's register budget must allow (experiment: 5)
-#ifndef RT_RES_OCC
-#define RT_RES_OCC 4
-#endif
-constexpr int kResOcc = RT_RES_OCC;
 
 // A lane's throughput T and radiance L in the wave's LDS block, [component][lane]
 // (the 4-wave resumable kernel).  The lane index is re-derived (stack_lane), so
 // it is not held in a register across the traversal either.
-#ifdef RT_NO_LDS_TL  // ablation build: T and L in registers
-constexpr bool kNoLdsTL = true;
-#else
-constexpr bool kNoLdsTL = false;
-#endif
 RT_D void tl_store(double* s_tl, V3 T, V3 L) {
     const uint32_t l = stack_lane();
     s_tl[l] = T.x; s_tl[kWave + l] = T.y; s_tl[2 * kWave + l] = T.z;
@@ -1520,7 +1348,7 @@ RT_D void tl_load(const double* s_tl, V3& T, V3& L) {
 }
 
 template <bool ST, bool HIT, int WAVES, bool RES, int KM = 3, bool CMP = false>
-__global__ __launch_bounds__(kWave, (RES && WAVES == 4) ? kResOcc : WAVES) void path_kernel(DevScene Sv, KParams Pv,
+__global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams Pv,
                                                      const DevScene* __restrict__ Sg,
                                                      const KParams* __restrict__ Pg, double* __restrict__ out,
                                                      double* __restrict__ part, int32_t* __restrict__ hit_ids,
@@ -1532,7 +1360,7 @@ __global__ __launch_bounds__(kWave, (RES && WAVES == 4) ? kResOcc : WAVES) void 
     // occupy registers (or scratch, where the 128-VGPR budget put them) across the
     // triangle traversal
     constexpr int kS = (RES && WAVES == 4) ? kShortRes : kShort;
-    constexpr bool kTL = RES && WAVES == 4 && !kNoLdsTL;
+    constexpr bool kTL = RES && WAVES == 4;
     __shared__ uint32_t s_n[kS * kWave];
     __shared__ double s_t[kS * kWave];
     __shared__ double s_tl[kTL ? 6 * kWave : 1];  // [T.x T.y T.z L.x L.y L.z][lane]
@@ -1540,9 +1368,6 @@ __global__ __launch_bounds__(kWave, (RES && WAVES == 4) ? kResOcc : WAVES) void 
     // camera rays of the next kCamSlots paths, [component][slot] (fused kernel only)
     __shared__ double s_cam[RES ? 1 : 3 * kCamSlots];
     __shared__ uint32_t s_uq[kUQ * kUW];  // open wave-tiles (store_unit)
-#ifdef RT_SUM_LDS  // experiment: the lane's committed-row sum in LDS instead of 6 VGPRs
-    __shared__ double s_sum[3 * kWave];
-#endif
     const uint32_t lane = threadIdx.x;
     auto stk = make_stack<RES, kS>(s_n, s_t, 0u, (uint64_t)blockIdx.x * kWave, spill_n, spill_t,
                                    gridDim.x * kWave);
@@ -1566,11 +1391,7 @@ __global__ __launch_bounds__(kWave, (RES && WAVES == 4) ? kResOcc : WAVES) void 
     const unsigned long long ph_tile = PH_T();
     if (lane < kRing) s_cnt[lane] = 0;
     __syncthreads();
-#ifdef RT_SUM_LDS
-    s_sum[lane] = 0.0; s_sum[kWave + lane] = 0.0; s_sum[2 * kWave + lane] = 0.0;
-#else
     V3 sum = v3(0.0, 0.0, 0.0);
-#endif
     uint32_t base = 0, next = 0, witers = 0;  // wave-uniform: next row to commit, next path to hand out
     uint32_t open_end = 0;                    // rows of the wave-tiles pulled so far
     uint32_t uq_front = 0, uq_back = 0;       // open wave-tiles: s_uq entries [uq_front, uq_back)
@@ -1589,13 +1410,8 @@ __global__ __launch_bounds__(kWave, (RES && WAVES == 4) ? kResOcc : WAVES) void 
         // (C3 at 64 spp: 315.6 vs 325.9 ms with the by-value kernel
         // arguments of the 4-wave kernel, whose loads were hoisted into
         // SGPRs and spilled)
-#ifndef RT_SCENE_BYVAL4  // ablation build: by-value arguments for the 4-wave kernel
-        constexpr bool kByPtr = true;
-#else
-        constexpr bool kByPtr = WAVES == 3;
-#endif
-        const DevScene& S = kByPtr ? *opaque(Sg) : Sv;
-        const KParams& P = kByPtr ? *opaque(Pg) : Pv;
+        const DevScene& S = *opaque(Sg);
+        const KParams& P = *opaque(Pg);
         const Scales sc{P.scale01, P.scale11};
         const uint64_t idle = __ballot(!busy);
         const unsigned long long ph_a = PH_T();
@@ -1756,12 +1572,7 @@ __global__ __launch_bounds__(kWave, (RES && WAVES == 4) ? kResOcc : WAVES) void 
         __syncthreads();
         while (base < open_end && s_cnt[base % kRing] == (uint32_t)kWave) {
             const double* rp = ring + ((uint64_t)(base % kRing) * kWave + lane) * 3;
-#ifdef RT_SUM_LDS
-            V3 sum = v3(s_sum[lane], s_sum[kWave + lane], s_sum[2 * kWave + lane]) + v3(rp[0], rp[1], rp[2]);
-            s_sum[lane] = sum.x; s_sum[kWave + lane] = sum.y; s_sum[2 * kWave + lane] = sum.z;
-#else
             sum = sum + v3(rp[0], rp[1], rp[2]);
-#endif
             __syncthreads();
             if (lane == 0) s_cnt[base % kRing] = 0;
             __syncthreads();
@@ -1774,11 +1585,7 @@ __global__ __launch_bounds__(kWave, (RES && WAVES == 4) ? kResOcc : WAVES) void 
                 const V3 res = own ? (Pt.chunks == 1 ? sum / (double)Pt.spp : sum) : v3(0.0, 0.0, 0.0);
                 double* o = (Pt.chunks == 1 ? out : part) + ((uint64_t)e[4] * kBlock + ly * RT_TILE + lx) * 3;
                 o[0] = res.x; o[1] = res.y; o[2] = res.z;
-#ifdef RT_SUM_LDS
-                s_sum[lane] = 0.0; s_sum[kWave + lane] = 0.0; s_sum[2 * kWave + lane] = 0.0;
-#else
                 sum = v3(0.0, 0.0, 0.0);
-#endif
                 ++uq_front;
             }
             ++base;
@@ -2045,11 +1852,9 @@ hipError_t launch_trace(const DevScene& S, const double* rays, uint32_t n, rt_hi
 // Experiment (variant builds only): a traversal-only persistent kernel for a
 // triangle-only scene on the compact layout — the trace half of a wavefront form.
 // It carries only the ray, its reciprocals and the traversal state, so it may run
-// more waves per SIMD (RT_WF_WAVES) with a KS-entry LDS stack.  Writes t and the
+// more waves per SIMD (kWfWaves) with a KS-entry LDS stack.  Writes t and the
 // global id of the closest triangle (rt_hit.t / .prim; the normals are not filled).
-#ifndef RT_WF_WAVES
-#define RT_WF_WAVES 6
-#endif
+constexpr int kWfWaves = 6;
 constexpr int kWfKS = 8;
 template <int WAVES, int KS>
 __global__ __launch_bounds__(kWave, WAVES) void trace_tri_kernel(DevScene S, const double* __restrict__ rays,
@@ -2104,7 +1909,7 @@ hipError_t launch_trace_tri(const DevScene& S, const double* rays, uint32_t n, r
                             uint32_t* spill_n, double* spill_t, uint32_t grid, hipStream_t st) {
     hipError_t e = hipMemsetAsync(queue, 0, kQueueWords * sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((trace_tri_kernel<RT_WF_WAVES, kWfKS>), dim3(grid), dim3(kWave), 0, st, S, rays, n, out, queue,
+    hipLaunchKernelGGL((trace_tri_kernel<kWfWaves, kWfKS>), dim3(grid), dim3(kWave), 0, st, S, rays, n, out, queue,
                        spill_n, spill_t);
     return hipGetLastError();
 }
@@ -2113,7 +1918,7 @@ hipError_t trace_tri_grid(uint32_t n, uint32_t* grid) {
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e == hipSuccess)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)trace_tri_kernel<RT_WF_WAVES, kWfKS>,
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)trace_tri_kernel<kWfWaves, kWfKS>,
                                                          kWave, 0);
     if (e != hipSuccess) return e;
     const uint64_t g = (uint64_t)std::max(per_cu, 1) * (uint64_t)std::max(cus, 1);

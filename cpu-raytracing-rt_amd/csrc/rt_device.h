@@ -208,11 +208,13 @@ RT_D bool gen_bool(Rng& r, double p) {  // Bernoulli
 struct Counters {
     uint32_t segments, aabb, tri, shape, shaded, lq, lhits, paths, steps;
     uint32_t lq_skip;  // last-bounce light queries the timed kernel skips (DevScene::lq_boxes)
+    uint32_t kids[3];  // inner-node visits of closest-hit traversals by child boxes hit: none, one, both
 };
 template <bool ON>
 struct Cnt {
     Counters c;
-    RT_D void zero() { if (ON) { c = Counters{0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; } }
+    RT_D void zero() { if (ON) { c = Counters{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, {0, 0, 0}}; } }
+    RT_D void kids(bool l, bool r) { if (ON) c.kids[(l ? 1 : 0) + (r ? 1 : 0)]++; }
     RT_D void lqskip() { if (ON) c.lq_skip++; }
     RT_D void segment() { if (ON) c.segments++; }
     RT_D void aabb(uint32_t n = 1) { if (ON) c.aabb += n; }
@@ -354,9 +356,7 @@ RT_D bool aabb_hit_fast(V3 mn, V3 mx, V3 o, const Rcp3& rc, V3 d, double& t) {
 }
 template <bool FAST = false>
 RT_D bool aabb_hit(V3 mn, V3 mx, V3 o, V3 d, const Rcp3& rc, double& t) {
-#ifndef RT_SLOW_AABB  // ablation build: the literal form for FAST too
     if (FAST) return aabb_hit_fast(mn, mx, o, rc, d, t);
-#endif
     if (!FAST && ((d.x == 0.0 && (o.x < mn.x || mx.x < o.x)) || (d.y == 0.0 && (o.y < mn.y || mx.y < o.y)) ||
                   (d.z == 0.0 && (o.z < mn.z || mx.z < o.z))))
         return false;
@@ -390,9 +390,6 @@ RT_D bool aabb_hit(V3 mn, V3 mx, V3 o, V3 d, const Rcp3& rc, double& t) {
 // change (its sign depends on the others), so vectors with a zero or
 // non-finite component take the generic formula.  Bit-exact either way.
 RT_D bool is_identity(const Quat& q) {
-#ifdef RT_NO_FASTROT  // ablation build
-    return false;
-#endif
     return q.s == 1.0 && q.v.x == 0.0 && q.v.y == 0.0 && q.v.z == 0.0;
 }
 RT_D bool all_nonzero_finite(V3 v) {
@@ -537,24 +534,7 @@ RT_D bool tri_uvt_r(const TriRec& r, V3 o, V3 d, double& u, double& v, double& t
     if (fabs(det) < 1e-11) return false;
     const V3 c0 = cross(m1, m2), c1 = cross(m2, m0), c2 = cross(m0, m1);
     V3 x0, x1, x2;
-#ifdef RT_TRI_QUOT
-    // The nine quotients c / det by the split division (dev_rcp once, dev_quotz per
-    // component): the same bits as c / det when det is in dir_ok's range and every
-    // dividend is 0 or in [2^-500, 2^402] (see "exact division"); taken when every
-    // lane testing a triangle here satisfies it, the plain division otherwise.
-    auto qok = [](double x) { const double a = fabs(x); return x == 0.0 || (a >= 0x1p-500 && a <= 0x1p402); };
-    const bool ok = dir_ok(det) && qok(c0.x) && qok(c0.y) && qok(c0.z) && qok(c1.x) && qok(c1.y) && qok(c1.z) &&
-                    qok(c2.x) && qok(c2.y) && qok(c2.z);
-    if (__ballot(!ok) == 0) {
-        const double rd = dev_rcp(det);
-        auto dq = [&](V3 c) { return v3(dev_quotz(c.x, det, rd), dev_quotz(c.y, det, rd), dev_quotz(c.z, det, rd)); };
-        x0 = dq(c0); x1 = dq(c1); x2 = dq(c2);
-    } else
-#endif
-    {
-        auto dv = [&](V3 c) { return c / det; };
-        x0 = dv(c0); x1 = dv(c1); x2 = dv(c2);
-    }
+    x0 = c0 / det; x1 = c1 / det; x2 = c2 / det;
     V3 w = o - r.a;
     double uu = dot(x0, w), vv = dot(x1, w), tt = dot(x2, w);
     if (uu < 0.0 || vv < 0.0 || 1.0 < uu + vv || tt < 0.0) return false;
@@ -562,7 +542,6 @@ RT_D bool tri_uvt_r(const TriRec& r, V3 o, V3 d, double& u, double& v, double& t
     return true;
 }
 RT_D bool tri_uvt(const DevTri& tr, V3 o, V3 d, double& u, double& v, double& t) {
-#ifndef RT_TRI_LAZY  // ablation build: per-field loads
     // The whole record in one batch of 16-B loads; the asm keeps `a` from being
     // loaded only after the determinant and its early exit, which exposed a second
     // memory round trip per test (C3 -1.3%, C5 -1.4% at reduced spp,
@@ -570,9 +549,6 @@ RT_D bool tri_uvt(const DevTri& tr, V3 o, V3 d, double& u, double& v, double& t)
     const TriRec r = load_tri(tr);
     asm volatile("" ::"v"(r.a.x), "v"(r.a.y), "v"(r.a.z));
     return tri_uvt_r(r, o, d, u, v, t);
-#else
-    return tri_uvt_r(TriRec{load3(tr.a), load3(tr.ba), load3(tr.ca)}, o, d, u, v, t);
-#endif
 }
 
 // Intersection (intersections.rs:10-16)

@@ -317,34 +317,12 @@ void build_compact(const HostBvh& h, const std::vector<TriItem>& items, HostBvhA
         if (!f32_exact3(n.box.min) || !f32_exact3(n.box.max)) return;
     for (const TriItem& it : items)
         if (!f32_exact3(it.t.a) || !f32_exact3(it.b) || !f32_exact3(it.c)) return;
-    // Record slots.  Pre-order (the reference's numbering, bvh.rs:104): a node and
-    // its left child share a 128-B line half the time.  RT_SIBLING_PAIRS
-    // (experiment): the two children of a node share one line (slots 2k, 2k + 1),
-    // pairs allocated in pre-order, so a far child popped after its sibling's
-    // subtree finds its record in the line the near descent fetched.  Only the
-    // addresses differ: the child words carry the slots, the root stays slot 0.
+    // Record slots: pre-order (the reference's numbering, bvh.rs:104), so a node and
+    // its left child share a 128-B line half the time.  (Pairing siblings in one line
+    // was measured neutral in round 3.)
     std::vector<uint32_t> slot(h.nodes.size());
     size_t n_slots = h.nodes.size();
-#ifdef RT_SIBLING_PAIRS
-    {
-        uint32_t next = 2;  // slot 1 pads the root's line
-        slot[0] = 0;
-        std::vector<uint32_t> st{0};
-        while (!st.empty()) {
-            const uint32_t i = st.back();
-            st.pop_back();
-            const HostNode& n = h.nodes[i];
-            if (n.left < 0) continue;
-            slot[n.left] = next; slot[n.right] = next + 1;
-            next += 2;
-            st.push_back((uint32_t)n.right);
-            st.push_back((uint32_t)n.left);
-        }
-        n_slots = next;
-    }
-#else
     for (size_t i = 0; i < h.nodes.size(); ++i) slot[i] = (uint32_t)i;
-#endif
     if (n_slots >= kLeafRef) return;
     std::vector<DevNodeC> cn(n_slots);
     std::memset(cn.data(), 0, n_slots * sizeof(DevNodeC));

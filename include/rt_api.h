@@ -185,9 +185,13 @@ typedef struct rt_scene_info {
     /* RT_LAYOUT_COMPACT_TRIS: the triangle BVH also has its compact layout (f32
        child boxes and vertices, every one an exact copy of the f64 value; DESIGN.md
        §2), which the resumable triangle-only kernel reads */
+    /* RT_LAYOUT_LQ_SKIP: every light is a box whose world bounds the host could
+       bound exactly (api.cpp lq_boxes), so the timed kernel may skip
+       last-bounce light queries proven NaN-free */
     uint32_t layout_flags;
 } rt_scene_info;
 #define RT_LAYOUT_COMPACT_TRIS 0x1u
+#define RT_LAYOUT_LQ_SKIP      0x2u
 int rt_scene_get_info(const rt_scene* scene, rt_scene_info* out);
 
 /* Kernel form of a scene's renders.  The library picks every
@@ -199,12 +203,16 @@ typedef struct rt_tuning {
     uint32_t waves;          /* 0 auto (4 when the BVHs hold > 4096 nodes, else 3); 3 or 4 waves/SIMD  */
     int32_t  resume;         /* -1 auto (1 for a triangle BVH of > 4096 nodes); 0 fused segment,
                                 1 resumable triangle traversal                                          */
-    uint32_t kinds;          /* 0 auto (the scene's primitive kinds); 3 the all-kinds instance          */
+    uint32_t kinds;          /* 0 auto (the scene's primitive kinds); 3 the all-kinds instance; 1 or 2
+                                only as the scene's own kinds (the value rt_scene_get_tuning reports)   */
     uint32_t suspend_lanes;  /* 0 auto (24 cache-resident BVH, 40 HBM-streamed); 1..64                   */
     uint32_t leaf_lanes;     /* 0 auto (32 cache-resident BVH, 24 HBM-streamed); 1..64                   */
-    uint32_t chunk_spp;      /* 0 the frame's rule (rt_sample_chunks); else the sample run length        */
+    uint32_t chunk_spp;      /* 0 the frame's rule (rt_sample_chunks); else the sample run length,
+                                raised if need be to <= 64 runs and <= 4 GiB of partial sums
+                                (rt_scene_sample_chunks reports the run length used)                    */
     int32_t  compact;        /* -1 auto (1 when the scene has it: RT_LAYOUT_COMPACT_TRIS); 0 the f64
-                                triangle-BVH layout; 1 the compact one (triangle-only resumable kernel) */
+                                triangle-BVH layout; 1 the compact one (triangle-only resumable kernel;
+                                RT_ERR_UNSUPPORTED on a scene without RT_LAYOUT_COMPACT_TRIS)           */
     uint32_t _reserved;
 } rt_tuning;
 /* NULL restores every field to auto.  Fields out of range -> RT_ERR_INVALID. */
@@ -238,7 +246,9 @@ int rt_render_tiles_async(rt_scene* scene, const rt_render_params* params,
 /* Diagnostics: the scene's raw device counter words (n <= 48), accumulated by
    RT_FLAG_STATS renders: words 0..9 are rt_stats' counters; word 10 counts the
    last-bounce light queries the timed (no-stats) kernel skips because they cannot
-   be NaN (the stats render still runs them); builds compiled
+   be NaN (the stats render still runs them); words 11..13
+   count the inner-node visits of closest-hit BVH traversals whose two child boxes
+   were hit by none / one / both slab tests; builds compiled
    with -DRT_PHASES add wave cycles and loop counts per path-kernel region at
    words 16..46 (tools/phases.py).  Not needed to render. */
 int rt_read_raw_stats(rt_scene* scene, uint64_t* out, uint32_t n);

@@ -269,6 +269,39 @@ def test_last_bounce_nan_box_light(sink_boxlight):
     assert g.read_raw_stats(11)[10] > 0
 
 
+def _sink_light_rotation(rt, orc, scene_text, rotation):
+    """The box-light kitchen sink with its light box's ROTATION line replaced."""
+    text = scene_text("kitchen_sink.txt")
+    lines, seen = [], 0
+    for line in text.split("\n"):
+        if line.startswith("EMISSION"):
+            seen += 1
+            if seen > 1:
+                continue
+        lines.append(line)
+    text = "\n".join(lines).replace("ROTATION 0.1 0.2 0 0.97467943448089633\nEMISSION",
+                                     f"ROTATION {rotation}\nEMISSION", 1)
+    assert f"ROTATION {rotation}" in text
+    desc, params = rt.parse_scene(text)
+    return desc, params, rt.Scene(desc), orc.OracleScene(desc)
+
+
+@pytest.mark.parametrize("rotation,skips", [("0.1 0.2 0 0.9747", True), ("0.3 0.6 0 1.1", False)])
+def test_last_bounce_skip_nonunit_light_rotation(rt, orc, scene_text, rotation, skips):
+    """A light box whose ROTATION is not a unit quaternion (printed to 4 digits: |q|^2 =
+    1.00004; or far from unit: 1.66).  cgmath's rotate_vector is then n R + (1 - n) I,
+    not a rotation, and the light's true world box is pos + M^-1(+-h) (api.cpp lq_boxes
+    inverts the model-space map instead of assuming R).  Near-unit: the skip stays on
+    and the frame is bit-exact with the oracle, NaN places included; far from unit:
+    the host turns the skip off (RT_LAYOUT_LQ_SKIP clear, no query skipped)."""
+    desc, params, g, o = _sink_light_rotation(rt, orc, scene_text, rotation)
+    assert bool(g.info()["layout_flags"] & 2) == skips
+    for depth in (2, 3):
+        _compare(g, o, params.replace(width=32, height=24, spp=48, ray_depth=depth, seed=10))
+    g.generate_image(params.replace(width=32, height=24, spp=4, ray_depth=3), stats=True)
+    assert (g.read_raw_stats(11)[10] > 0) == skips
+
+
 def test_kitchen_sink_deep(sink):
     desc, params, g, o = sink
     _compare(g, o, params.replace(width=24, height=20, spp=3, ray_depth=24, seed=99))
@@ -502,7 +535,7 @@ def test_deep_stack_and_big_leaf_render(rt, orc):
     desc.tri_vertices = desc.tri_vertices.astype(np.float32).astype(np.float64)
     g, o = rt.Scene(desc), orc.OracleScene(desc)
     info = g.info()
-    assert info["layout_flags"] == 1 and info["bvh_depth"][2] > 12 + 6
+    assert info["layout_flags"] & 1 and info["bvh_depth"][2] > 12 + 6
     f = np.array([0.0, -0.4, 1.0]) / np.sqrt(1.16)
     u = np.array([0.0, 1.0, 0.4]) / np.sqrt(1.16)
     p = rt.RenderParams(width=24, height=16, spp=2, ray_depth=4, cam_position=(0.0, 0.5, -1.0),

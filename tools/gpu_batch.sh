@@ -103,6 +103,11 @@ for s in $STEPS; do
       run calib_dram 120 rocprofv3 --pmc TCC_EA0_RDREQ_DRAM_sum TCC_HIT_sum TCC_MISS_sum --output-format csv \
         -d "$OUT/calib_dram" -o run -- tools/fetch_calib || exit 1
       run calib_report 60 python3 tools/fetch_calib.py "$OUT" || exit 1 ;;
+    c5t)   run pytest_c5 900 python3 -u -m pytest tests/test_gpu_c5.py -m gpu -x -v --timeout 600 \
+             --timeout-method thread || exit 1 ;;
+    kids)  run kid_stats 600 python3 tools/kid_stats.py C3 64 C5 16 || exit 1 ;;
+    valu)  run valu_rates 300 tools/valu_rates full || exit 1 ;;
+    *)     echo "unknown step $s"; exit 2 ;;
   esac
 done
 echo "[$(date +%T)] batch done"

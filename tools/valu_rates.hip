@@ -21,11 +21,18 @@
 constexpr int kIters = 16384;  // loop trips; 8 instructions each
 
 enum Op { FMA64, ADD64, MUL64, MAX64, RCP64, CMP64, FMA32, ADD32F, ADDU32, CNDMASK, MADU64, DIV64, SQRT64,
-          LAT_FMA64, LAT_FMA32, LAT_RCP64, NOPS };
+          LAT_FMA64, LAT_FMA32, LAT_RCP64,
+          // round 4: the classes outside the f64 / int64 PMC counters ("other" in bench.py)
+          MOV32, DPP, RFL, CVT64F32, CVT32F64, AND32, LSHL32, MULLO32, CMPU32, CMPCLS64, BFE32, ADDCO32,
+          DIVSCALE64, DIVFMAS64, DIVFIXUP64, CNDMASK_VCC, NOPS };
 static const char* kName[NOPS] = {"v_fma_f64", "v_add_f64", "v_mul_f64", "v_max_f64", "v_rcp_f64",
                                   "v_cmp_lt_f64", "v_fma_f32", "v_add_f32", "v_add_u32", "v_cndmask_b32",
                                   "v_mad_u64_u32", "f64 x/y (compiled)", "f64 sqrt (compiled)",
-                                  "dependent v_fma_f64", "dependent v_fma_f32", "dependent v_rcp_f64"};
+                                  "dependent v_fma_f64", "dependent v_fma_f32", "dependent v_rcp_f64",
+                                  "v_mov_b32", "v_mov_b32_dpp", "v_readfirstlane_b32", "v_cvt_f64_f32",
+                                  "v_cvt_f32_f64", "v_and_b32", "v_lshlrev_b32", "v_mul_lo_u32", "v_cmp_gt_u32",
+                                  "v_cmp_class_f64", "v_bfe_u32", "v_add_co_u32", "v_div_scale_f64",
+                                  "v_div_fmas_f64", "v_div_fixup_f64", "v_cndmask_b32 (vcc)"};
 
 #define R8(S) S S S S S S S S
 
@@ -94,6 +101,44 @@ __global__ __launch_bounds__(256) void rate_kernel(double* out, unsigned long lo
             asm volatile(INS : "+v"(q6) : "v"(u1) : "vcc"); asm volatile(INS : "+v"(q7) : "v"(u1) : "vcc");
             Q8("v_mad_u64_u32 %0, vcc, %1, %1, %0")
         }
+        if constexpr (OP == MOV32) { U8("v_mov_b32 %0, %1") }
+        if constexpr (OP == DPP) { U8("v_mov_b32_dpp %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf") }
+        if constexpr (OP == RFL) {
+            unsigned s0, s1, s2, s3, s4, s5, s6, s7;
+            asm volatile(R8("v_readfirstlane_b32 %0, %8\n") "s_nop 0\n"
+                         : "=s"(s0), "=s"(s1), "=s"(s2), "=s"(s3), "=s"(s4), "=s"(s5), "=s"(s6), "=s"(s7)
+                         : "v"(u0));
+            u0 += s0 ^ s7;
+        }
+        if constexpr (OP == CVT64F32) {
+            asm volatile(R8("v_cvt_f64_f32 %0, %1\n") : "=v"(a0) : "v"(f0));
+            a1 += a0;
+        }
+        if constexpr (OP == CVT32F64) {
+            asm volatile(R8("v_cvt_f32_f64 %0, %1\n") : "=v"(f0) : "v"(a0));
+            f1 += f0;
+        }
+        if constexpr (OP == AND32) { U8("v_and_b32 %0, %0, %1") }
+        if constexpr (OP == LSHL32) { U8("v_lshlrev_b32 %0, 3, %1") }
+        if constexpr (OP == MULLO32) { U8("v_mul_lo_u32 %0, %0, %1") }
+        if constexpr (OP == CMPU32) { asm volatile(R8("v_cmp_gt_u32 vcc, %0, %1\n") : : "v"(u0), "v"(u1) : "vcc"); }
+        if constexpr (OP == CMPCLS64) {
+            asm volatile(R8("v_cmp_class_f64 vcc, %0, %1\n") : : "v"(a0), "v"(u1) : "vcc");
+        }
+        if constexpr (OP == BFE32) { U8("v_bfe_u32 %0, %0, 3, 7") }
+        if constexpr (OP == ADDCO32) {
+            asm volatile(R8("v_add_co_u32 %0, vcc, %0, %1\n") : "+v"(u0) : "v"(u1) : "vcc");
+        }
+        if constexpr (OP == DIVSCALE64) { D8("v_div_scale_f64 %0, vcc, %1, %1, %0") }
+        if constexpr (OP == DIVFMAS64) {
+            asm volatile("s_mov_b64 vcc, 0" ::: "vcc");
+            D8("v_div_fmas_f64 %0, %0, %1, %2")
+        }
+        if constexpr (OP == DIVFIXUP64) { D8("v_div_fixup_f64 %0, %0, %1, %2") }
+        if constexpr (OP == CNDMASK_VCC) {
+            asm volatile("s_mov_b64 vcc, %0" :: "s"(mask) : "vcc");
+            U8("v_cndmask_b32 %0, %0, %1, vcc")
+        }
         if constexpr (OP == DIV64) {
             a0 = m / a0; a1 = m / a1; a2 = m / a2; a3 = m / a3; a4 = m / a4; a5 = m / a5; a6 = m / a6; a7 = m / a7;
         }
@@ -113,8 +158,9 @@ __global__ __launch_bounds__(256) void rate_kernel(double* out, unsigned long lo
     }
 }
 
+static int cus = 0;
 template <int OP>
-static void run(int waves_per_simd, int cus) {
+static void run(int waves_per_simd, int /*unused*/) {
     const int blocks = cus * waves_per_simd;  // 256 threads = one wave per SIMD per block
     const int nw = blocks * 4;
     double* out; unsigned long long *cyc, *rt;
@@ -137,19 +183,34 @@ static void run(int waves_per_simd, int cus) {
     for (int i = 0; i < nw; ++i) { mc += (double)c[i]; mr += (double)r[i]; }
     mc /= nw; mr /= nw;
     const double per_wave = 8.0 * kIters;  // instructions (or operations) per wave
-    const double cpi = mc / (waves_per_simd * per_wave);  // cycles per wave-instruction per SIMD (all its waves)
     const double ghz = mc / (mr * 10.0);                // s_memrealtime ticks at 100 MHz
-    // chip-wide rate from wall time: wave-instructions per second
+    // chip-wide rate from wall time: wave-instructions per second; and the SIMD issue
+    // cycles per wave-instruction it implies at the in-kernel clock (the waves of one
+    // SIMD do not all run the whole launch side by side, so each wave's own s_memtime
+    // span under-counts: the wall form is the issue cost, round 4)
     const double wall_rate = (double)nw * per_wave / (ms * 1e-3);
+    const double cpi = ghz * 1e9 * (double)(cus * 4) / wall_rate;
     printf("%-22s waves/SIMD %d  cycles/wave-instr/SIMD %6.2f  clock %.3f GHz  wall %.3f ms  %.3e wave-instr/s\n",
            kName[OP], waves_per_simd, cpi, ghz, ms, wall_rate);
     CK(hipFree(out)); CK(hipFree(cyc)); CK(hipFree(rt));
 }
 
-int main() {
-    int cus = 0;
+int main(int argc, char** argv) {
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     printf("CUs %d\n", cus);
+    if (argc > 1) {  // round 4: the full-load (8 waves/SIMD) table of every class, for bench.py's pricing
+        run<FMA64>(8, cus); run<ADD64>(8, cus); run<MUL64>(8, cus); run<MAX64>(8, cus); run<RCP64>(8, cus);
+        run<CMP64>(8, cus); run<FMA32>(8, cus); run<ADD32F>(8, cus); run<ADDU32>(8, cus); run<CNDMASK>(8, cus);
+        run<MADU64>(8, cus); run<MOV32>(8, cus); run<DPP>(8, cus); run<RFL>(8, cus); run<CVT64F32>(8, cus);
+        run<CVT32F64>(8, cus); run<AND32>(8, cus); run<LSHL32>(8, cus); run<MULLO32>(8, cus); run<CMPU32>(8, cus);
+        run<CMPCLS64>(8, cus); run<BFE32>(8, cus); run<ADDCO32>(8, cus); run<DIVSCALE64>(8, cus);
+        run<DIVFMAS64>(8, cus); run<DIVFIXUP64>(8, cus); run<CNDMASK_VCC>(8, cus);
+        for (int w : {4}) {
+            run<FMA64>(w, cus); run<CMP64>(w, cus); run<CNDMASK>(w, cus); run<MOV32>(w, cus); run<DPP>(w, cus);
+            run<RFL>(w, cus); run<CVT64F32>(w, cus); run<AND32>(w, cus); run<CMPU32>(w, cus);
+        }
+        return 0;
+    }
     // dependent-chain latency: one chain, one wave per SIMD
     run<LAT_FMA64>(1, cus); run<LAT_FMA32>(1, cus); run<LAT_RCP64>(1, cus);
     for (int w : {1, 2, 4, 8}) {
