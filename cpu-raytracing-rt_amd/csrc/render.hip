@@ -928,6 +928,15 @@ RT_D double lights_impact(const DevScene& S, V3 o, V3 d, Stk& stk, Cnt<ST>& C, u
     if (KM & kTris) bvh_all<3, ST>(S.ltris, o, d, rc, rfast, stk, C, impact, nhits);
     return impact;
 }
+// the same query from its origin q = pos + dir * kEpsilon, already computed
+template <bool ST, class Stk, int KM = 3>
+RT_D double light_pdf_at(const DevScene& S, V3 q, V3 dir, Stk& stk, Cnt<ST>& C) {
+    C.lq();
+    uint32_t nh = 0;
+    double impact = lights_impact<ST, Stk, KM>(S, q, dir, stk, C, nh);
+    const uint32_t nl = S.n_lights;  // x / 1 == x exactly: skip the division sequence for one light
+    return nl == 1u ? impact : impact / (double)nl;
+}
 template <bool ST, class Stk, int KM = 3>
 RT_D double light_pdf(const DevScene& S, V3 pos, V3 dir, Stk& stk, Cnt<ST>& C) {  // ray_sampler.rs:132-139
     C.lq();
@@ -1071,23 +1080,58 @@ RT_D void segment_begin(const DevScene& S, const PathState& ps, Stk& stk, Cnt<ST
     trav_init<2, ST>(S.tris, ps.o, ps.d, q.rc, q.fast, stk, C, q.T);
 }
 
+// A lane's throughput T and radiance L in the wave's LDS block, [component][lane]
+// (the 4-wave resumable kernel).  The lane index is re-derived (stack_lane), so
+// it is not held in a register across the traversal either.  The shading step
+// updates them in place (tl_add_L, tl_mul_T) where the reference does, so they
+// occupy no registers while the light query and the samplers run (round 4).
+RT_D void tl_store(double* s_tl, V3 T, V3 L) {
+    const uint32_t l = stack_lane();
+    s_tl[l] = T.x; s_tl[kWave + l] = T.y; s_tl[2 * kWave + l] = T.z;
+    s_tl[3 * kWave + l] = L.x; s_tl[4 * kWave + l] = L.y; s_tl[5 * kWave + l] = L.z;
+}
+RT_D V3 tl_L(const double* s_tl) {
+    const uint32_t l = stack_lane();
+    return v3(s_tl[3 * kWave + l], s_tl[4 * kWave + l], s_tl[5 * kWave + l]);
+}
+
+RT_D void tl_add_L(double* s_tl, V3 e) {  // L = L + T (x) e
+    const uint32_t l = stack_lane();
+    const V3 T = v3(s_tl[l], s_tl[kWave + l], s_tl[2 * kWave + l]);
+    s_tl[3 * kWave + l] = s_tl[3 * kWave + l] + T.x * e.x;
+    s_tl[4 * kWave + l] = s_tl[4 * kWave + l] + T.y * e.y;
+    s_tl[5 * kWave + l] = s_tl[5 * kWave + l] + T.z * e.z;
+}
+RT_D void tl_mul_T(double* s_tl, V3 w) {  // T = T (x) w
+    const uint32_t l = stack_lane();
+    s_tl[l] = s_tl[l] * w.x; s_tl[kWave + l] = s_tl[kWave + l] * w.y; s_tl[2 * kWave + l] = s_tl[2 * kWave + l] * w.z;
+}
+RT_D void tl_nan_L(double* s_tl) {
+    const uint32_t l = stack_lane();
+    s_tl[3 * kWave + l] = NAN; s_tl[4 * kWave + l] = NAN; s_tl[5 * kWave + l] = NAN;
+}
+
 // One segment of raytrace_impl (raytrace.rs:12-60) in throughput form, from
 // the closest-hit result on.  Returns true when the path continues with the
 // updated ray.  `last`: this is the path's last segment (raytrace_impl with
 // left == 1).
-template <bool ST, class Stk, bool SLT = false, int KM = 3>
+// LT: the path's T and L live in the wave's LDS (s_tl; the 4-wave resumable
+// kernel), updated in place; ps.T / ps.L are not used.
+template <bool ST, class Stk, bool SLT = false, int KM = 3, bool LT = false>
 RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, PathState& ps, Rng& rng,
                         Stk& stk, Cnt<ST>& C, bool hit, const Hit& h, uint32_t mat, int32_t gid,
-                        int32_t& hit_gid, bool more, bool last) {
+                        int32_t& hit_gid, bool more, bool last, double* s_tl = nullptr) {
     if (!hit) {
         hit_gid = RT_HIT_MISS;
-        ps.L = ps.L + mul(ps.T, load3(P.bg));
+        if (LT) tl_add_L(s_tl, load3(P.bg));
+        else ps.L = ps.L + mul(ps.T, load3(P.bg));
         return false;
     }
     hit_gid = gid;
     const DevMaterial& m = S.mats[mat];
     const V3 col = load3(m.color);
-    ps.L = ps.L + mul(ps.T, load3(m.emission));
+    if (LT) tl_add_L(s_tl, load3(m.emission));
+    else ps.L = ps.L + mul(ps.T, load3(m.emission));
     // The last segment shades like every other: its direction and pdf decide
     // whether raytrace_impl's last level is NaN (below).  (Stopping after the
     // emission, round 2, was 2.6% faster on C2 but misses that NaN.)
@@ -1118,6 +1162,30 @@ RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, P
         dir = degen ? h.ns : nrm(sw);
         const double cs = dot(dir, h.ns);
         if (cs <= 0.0) return false;
+        if (LT) {
+            // The light query's ray (pos + dir * eps, dir; ray_sampler.rs:132-139) IS the
+            // next segment's: set it first, so the old ray, the hit and the colour are dead
+            // while the query runs (the colour is re-read for the weight).
+            const double cp = cosine_pdf(h.ns, dir);
+            ps.o = pos + dir * kEpsilon;
+            ps.d = dir;
+            double lp = 0.0;
+            bool query = !empty;
+            if (KM != kTris && last && query && lq_skippable(S, ps.o)) {  // box lights only
+                C.lqskip();
+                query = ST;
+            }
+            if (query) {
+                const unsigned long long ph2 = PH_T();
+                lp = light_pdf_at<ST, Stk, KM>(S, ps.o, ps.d, stk, C);
+                PH_ADDW(kPhLightPdf, ph2);
+            }
+            const double pdf = empty ? cp : (cp + lp) / 2.0;  // Mix::pdf
+            if (pdf == 0.0) return false;
+            tl_mul_T(s_tl, diffuse_weight(load3(S.mats[mat].color), cp, pdf));
+            if (last && (isnan(cs) || isnan(pdf))) tl_nan_L(s_tl);  // see below
+            return true;
+        }
         if (SLT && more && uni_u32(S.slt_mask)) {
             // the light query's ray is the next segment's: defer the pdf to its box
             // tests.  cosine_pdf = cs / pi here (cs > 0); above 2^-1000 the Mix pdf
@@ -1180,7 +1248,10 @@ RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, P
                 const V3 tdir = d * k + h.ns * (k * cos1 - cos2);
                 ps.o = hp + tdir * kEpsilon;
                 ps.d = tdir;
-                if (!h.inside) ps.T = mul(ps.T, col);
+                if (!h.inside) {
+                    if (LT) tl_mul_T(s_tl, col);
+                    else ps.T = mul(ps.T, col);
+                }
             }
         }
         if (reflect) { ps.o = hp + rdir * kEpsilon; ps.d = rdir; }
@@ -1189,14 +1260,15 @@ RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, P
     // Metallic (:56-58)
     ps.o = hp + rdir * kEpsilon;
     ps.d = rdir;
-    ps.T = mul(ps.T, col);
+    if (LT) tl_mul_T(s_tl, col);
+    else ps.T = mul(ps.T, col);
     return true;
 }
 
 // the resumable form's end of a segment: finish `intersect`, then shade
-template <bool ST, int KM = 3, bool CMP = false, class Stk>
+template <bool ST, int KM = 3, bool CMP = false, bool LT = false, class Stk>
 RT_D bool segment_end(const DevScene& S, const KParams& P, const Scales& sc, PathState& ps, Rng& rng,
-                      Stk& stk, Cnt<ST>& C, SegQuery& q, int32_t& hit_gid, bool last) {
+                      Stk& stk, Cnt<ST>& C, SegQuery& q, int32_t& hit_gid, bool last, double* s_tl) {
     Hit h; uint32_t mat = 0; int32_t gid = 0;
     if (KM == kTris) {  // the candidate is the triangle traversal's (take_tri on an empty best)
         q.best.valid = false; q.best.t = 0.0; q.best.u = q.best.v = 0.0; q.best.prim = 0; q.best.aux = 0;
@@ -1204,7 +1276,8 @@ RT_D bool segment_end(const DevScene& S, const KParams& P, const Scales& sc, Pat
     }
     take_tri(q.best, q.T.valid, q.T.best, q.T.bu, q.T.bv, q.T.prim);
     const bool hit = intersect_tail<ST, KM>(S, q.best, ps.o, ps.d, C, h, mat, gid);
-    return segment_shade<ST, Stk, false, KM>(S, P, sc, ps, rng, stk, C, hit, h, mat, gid, hit_gid, false, last);
+    return segment_shade<ST, Stk, false, KM, LT>(S, P, sc, ps, rng, stk, C, hit, h, mat, gid, hit_gid, false, last,
+                                                 s_tl);
 }
 
 // the fused form: one whole segment (scene_intersect to completion, then shade)
@@ -1332,20 +1405,6 @@ RT_D uint32_t unit_of_row(const uint32_t* uq, uint32_t uq_back, uint32_t row) {
     return i % kUQ;
 }
 
-
-// A lane's throughput T and radiance L in the wave's LDS block, [component][lane]
-// (the 4-wave resumable kernel).  The lane index is re-derived (stack_lane), so
-// it is not held in a register across the traversal either.
-RT_D void tl_store(double* s_tl, V3 T, V3 L) {
-    const uint32_t l = stack_lane();
-    s_tl[l] = T.x; s_tl[kWave + l] = T.y; s_tl[2 * kWave + l] = T.z;
-    s_tl[3 * kWave + l] = L.x; s_tl[4 * kWave + l] = L.y; s_tl[5 * kWave + l] = L.z;
-}
-RT_D void tl_load(const double* s_tl, V3& T, V3& L) {
-    const uint32_t l = stack_lane();
-    T = v3(s_tl[l], s_tl[kWave + l], s_tl[2 * kWave + l]);
-    L = v3(s_tl[3 * kWave + l], s_tl[4 * kWave + l], s_tl[5 * kWave + l]);
-}
 
 template <bool ST, bool HIT, int WAVES, bool RES, int KM = 3, bool CMP = false>
 __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams Pv,
@@ -1527,15 +1586,9 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
                 if (inq) {
                     int32_t g;
                     const unsigned long long ph_s = PH_T();
-                    if constexpr (kTL) {
-                        tl_load(s_tl, ps.T, ps.L);
-                        rng_rekey(rng, P.seed);
-                    }
-                    cont = segment_end<ST, KM, CMP>(S, P, sc, ps, rng, stk, C, q, g, b + 1 >= depth);
-                    if constexpr (kTL) {
-                        tl_store(s_tl, ps.T, ps.L);
-                        rng_park(rng);
-                    }
+                    if constexpr (kTL) rng_rekey(rng, P.seed);
+                    cont = segment_end<ST, KM, CMP, kTL>(S, P, sc, ps, rng, stk, C, q, g, b + 1 >= depth, s_tl);
+                    if constexpr (kTL) rng_park(rng);
                     PH_ADDW(kPhSegment, ph_s);
                     if (HIT) hit_ids[(pixel * P.spp + s) * depth + b] = g;
                     ++b;
@@ -1560,7 +1613,7 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
             if (HIT) for (uint32_t k = b; k < depth; ++k) hit_ids[(pixel * P.spp + s) * depth + k] = RT_HIT_NONE;
             const uint32_t r = (cur / kWave) % kRing;
             double* rp = ring + ((uint64_t)r * kWave + cur % kWave) * 3;
-            if constexpr (kTL) { V3 t; tl_load(s_tl, t, ps.L); }
+            if constexpr (kTL) ps.L = tl_L(s_tl);
             rp[0] = ps.L.x; rp[1] = ps.L.y; rp[2] = ps.L.z;
             atomicAdd(&s_cnt[r], 1u);
             busy = false;
