@@ -79,24 +79,41 @@ def algo_bytes(st):
 PATH_KERNEL = "path_kernel<false, false,"  # the timed instance (any waves/SIMD budget)
 
 # VALU issue roofline.  The path kernel is f64 VALU-issue bound,
-# not HBM- or MFMA-bound.  Issue cost of one wave64 VALU instruction on a gfx950
-# SIMD, in shader cycles: 2 for 32-bit ops (MI355X_MICROARCH.md "Wave
-# scheduling": 32 lanes/cycle x 2), and from tools/valu_rates.hip with every
-# SIMD loaded (profiles/r02/valu_rates.log, 8 waves/SIMD): v_fma/mul/add_f64
-# 4.2, v_rcp_f64 16.2, v_mad_u64_u32 4.5.  Instructions outside the counted
-# classes (compares, cndmask, moves, f32, int32) are priced at the 2-cycle
-# floor, although v_cmp_*_f64 and v_cndmask_b32 measure ~4: the busy fraction
-# below is therefore a LOWER bound.
+# not HBM- or MFMA-bound.  Every PMC class of VALU instruction is priced in SIMD
+# issue cycles per wave64 instruction, measured at full load (8 waves/SIMD, wall
+# clock; tools/valu_rates.hip, profiles/r04/valu_rates_full.log): v_fma/mul/add_f64
+# 4.2, f64 transcendentals 16.2, int64 (v_mad_u64_u32, v_lshl_add_u64) 4.5.  The
+# classes without a single rate — int32 (v_add_u32 2.3 ... v_lshlrev / v_bfe /
+# v_mul_lo 4.2), conversions, f32, and the uncounted rest (v_cmp_*, v_cndmask,
+# moves, readlane: 2.3 ... 4.2) — take the mean measured cost of their opcodes
+# weighted by the kernel instance's static code (tools/valu_mix.py ->
+# tools/valu_prices.json: rest 4.0, int32 2.8, cvt 4.4).  frac is priced
+# that way; frac_lower / frac_upper price every class without its own rate at the
+# cheapest (2.3) / dearest (4.2) measured 32-bit cost.
 SIMDS = 256 * 4
 MAX_CLOCK_HZ = 2.4e9
-VALU_CYCLES = {"f64": 4.0, "trans_f64": 16.0, "int64": 4.0, "other": 2.0}
+VALU_CYCLES = {"f64": 4.2, "trans_f64": 16.2, "int64": 4.5}
+CHEAP, DEAR = 2.3, 4.2
+PRICES_FILE = os.path.join(HERE, "tools", "valu_prices.json")  # profiles/ does not travel to the box
 PMC_PASSES = (
     # (counters, one pass each: <= 8 SQ, <= 4 TCC (FETCH_SIZE uses 3, WRITE_SIZE 2), <= 2 GRBM)
     ("FETCH_SIZE", "SQ_THREAD_CYCLES_VALU", "SQ_ACTIVE_INST_VALU"),
     ("WRITE_SIZE",),
     ("SQ_INSTS_VALU", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64",
      "SQ_INSTS_VALU_TRANS_F64", "SQ_INSTS_VALU_INT64", "GRBM_GUI_ACTIVE"),
+    ("SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_CVT", "SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32",
+     "SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_TRANS_F32"),
 )
+
+
+def class_prices(instance):
+    """Static-mix mean prices of the int32 / cvt / f32 / rest classes for one kernel
+    instance (tools/valu_mix.py); None when the table is absent."""
+    try:
+        d = json.load(open(PRICES_FILE))["instances"][instance]["classes"]
+    except (OSError, KeyError, ValueError):
+        return None
+    return {k: d[k]["mean_cycles"] for k in ("int32", "cvt", "f32", "rest") if k in d}
 
 
 DIST_ENV = ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
@@ -180,19 +197,29 @@ def hbm_traffic(pmc):
                            "kernel": PATH_KERNEL}
 
 
-def valu_roofline(pmc, pmc_ns, kern_s):
-    """VALU issue roofline of the path kernel: wave-instructions per second over
-    the instruction-mix-weighted issue limit of the chip's 1024 SIMDs."""
+def valu_roofline(pmc, pmc_ns, kern_s, instance):
+    """VALU issue roofline of the path kernel: busy SIMD issue cycles of the launch's
+    instruction mix (every PMC class at its measured price) over the cycles the
+    chip's 1024 SIMDs had during the launch."""
     n = pmc["SQ_INSTS_VALU"]
     f64 = pmc["SQ_INSTS_VALU_FMA_F64"] + pmc["SQ_INSTS_VALU_MUL_F64"] + pmc["SQ_INSTS_VALU_ADD_F64"]
     trans, i64 = pmc["SQ_INSTS_VALU_TRANS_F64"], pmc["SQ_INSTS_VALU_INT64"]
-    other = max(0.0, n - f64 - trans - i64)
-    busy = (VALU_CYCLES["f64"] * f64 + VALU_CYCLES["trans_f64"] * trans + VALU_CYCLES["int64"] * i64 +
-            VALU_CYCLES["other"] * other)  # SIMD issue cycles the launch needs
+    i32, cvt = pmc["SQ_INSTS_VALU_INT32"], pmc["SQ_INSTS_VALU_CVT"]
+    f32 = (pmc["SQ_INSTS_VALU_ADD_F32"] + pmc["SQ_INSTS_VALU_MUL_F32"] + pmc["SQ_INSTS_VALU_FMA_F32"] +
+           pmc["SQ_INSTS_VALU_TRANS_F32"])
+    rest = max(0.0, n - f64 - trans - i64 - i32 - cvt - f32)
+    mix = {"int32": i32, "cvt": cvt, "f32": f32, "rest": rest}
+    prices = class_prices(instance) or {}
+    priced = {k: prices.get(k, (CHEAP + DEAR) / 2) for k in mix}
+    fixed = VALU_CYCLES["f64"] * f64 + VALU_CYCLES["trans_f64"] * trans + VALU_CYCLES["int64"] * i64
+    busy = fixed + sum(priced[k] * mix[k] for k in mix)  # SIMD issue cycles the launch needs
+    lo = fixed + CHEAP * sum(mix.values())
+    hi = fixed + DEAR * sum(mix.values())
     # shader clock of the profiled launch: GRBM_GUI_ACTIVE is summed over the 8 XCDs
     clk = pmc["GRBM_GUI_ACTIVE"] / 8.0 / (pmc_ns * 1e-9) if pmc_ns else 0.0
     clk_used = clk if 1.0e9 <= clk <= MAX_CLOCK_HZ else MAX_CLOCK_HZ
-    frac = busy / (SIMDS * clk_used * kern_s)
+    avail = SIMDS * clk_used * kern_s
+    frac = busy / avail
     achieved = n / kern_s / 1e9
     lanes = pmc["SQ_THREAD_CYCLES_VALU"] / pmc["SQ_ACTIVE_INST_VALU"]
     return {
@@ -202,16 +229,23 @@ def valu_roofline(pmc, pmc_ns, kern_s):
         "unit": "G wave64 VALU instr/s",
         "frac": frac,
         "valu_detail": {
-            "instr_per_launch": n, "f64_fma_mul_add": f64, "f64_trans": trans, "int64": i64, "other": other,
-            "issue_cycles_per_instr": VALU_CYCLES, "busy_simd_cycles": busy,
+            "instr_per_launch": n, "f64_fma_mul_add": f64, "f64_trans": trans, "int64": i64, "int32": i32,
+            "cvt": cvt, "f32": f32, "rest": rest,
+            "issue_cycles_per_instr": {**VALU_CYCLES, **priced},
+            "prices_source": ("profiles/r04/valu_rates_full.log (measured, 8 waves/SIMD); int32/cvt/f32/rest: "
+                              f"static-mix means of {instance} (tools/valu_prices.json)"
+                              if prices else "int32/cvt/f32/rest at the mid of the measured 32-bit range"),
+            "busy_simd_cycles": busy,
+            "frac_lower": lo / avail, "frac_upper": hi / avail,
             "clock_GHz": clk_used / 1e9, "clock_measured_GHz": clk / 1e9,
             "active_lanes_per_instr": lanes, "lane_util": lanes / 64.0,
             "useful_lane_frac": frac * lanes / 64.0,
-            "hw_active_frac": 4.0 * pmc["SQ_ACTIVE_INST_VALU"] / (SIMDS * clk_used * kern_s),
+            "hw_active_frac": 4.0 * pmc["SQ_ACTIVE_INST_VALU"] / avail,
             "peak_note": "peak = the same instruction mix issued back to back on all 1024 SIMDs at the measured "
-                         "clock; frac = busy SIMD cycles / available (a lower bound: uncounted classes at the "
-                         "2-cycle floor); useful_lane_frac = frac x active lanes / 64 (divergence); "
-                         "hw_active_frac = SQ_ACTIVE_INST_VALU quad-cycles x 4 / available cycles",
+                         "clock; frac = busy SIMD cycles (every class at its measured issue cost) / available; "
+                         "frac_lower / frac_upper = the classes without their own rate at 2.3 / 4.2 cycles; "
+                         "useful_lane_frac = frac x active lanes / 64 (divergence); hw_active_frac = "
+                         "SQ_ACTIVE_INST_VALU quad-cycles x 4 / available cycles",
         },
     }
 
@@ -419,7 +453,8 @@ def main():
             roofline = {"bound": "valu", "achieved": None, "peak": None, "unit": "G wave64 VALU instr/s",
                         "frac": None, "traffic": None, "note": f"PMC passes unavailable: {pmc_ns}"}
         else:
-            roofline = valu_roofline(pmc, pmc_ns, kern_s)
+            roofline = valu_roofline(pmc, pmc_ns, kern_s, "C2" if scene.tuning()["kinds"] == 1 else
+                                     ("C3" if scene.tuning()["compact"] == 1 else "tri_f64"))
             traffic, detail = hbm_traffic(pmc)
             roofline["traffic"] = traffic
             roofline["hbm"] = {"achieved_GBps": traffic / kern_s / 1e9, "peak_GBps": HBM_PEAK_GBS,
@@ -443,7 +478,8 @@ def main():
         })
         out = {
             "metric": "Msamples/s (rays traced x bounces) at 1920x1080, 256 spp; fraction of f64 VALU-issue "
-                      "roofline (modelled lower bound; the measured HBM fraction is roofline.hbm)",
+                      "roofline (measured issue costs per instruction class; the measured HBM fraction is "
+                      "roofline.hbm)",
             "value": value,
             "unit": "Msamples/s",
             "n_gpus": world,

@@ -31,3 +31,21 @@ def test_pmc_child_leaves_the_process_group():
     assert out["HIP_VISIBLE_DEVICES"] == "3"
     # a single-process run has nothing to strip
     assert b.child_env({"PATH": "/usr/bin"}) == {"PATH": "/usr/bin"}
+
+
+def test_valu_roofline_prices_every_class():
+    """frac prices each PMC class at its measured issue cost (tools/valu_prices.json for the
+    classes without a single rate); the 2.3 / 4.2-cycle bounds bracket it."""
+    b = _bench()
+    pmc = {"SQ_INSTS_VALU": 100.0, "SQ_INSTS_VALU_FMA_F64": 20.0, "SQ_INSTS_VALU_MUL_F64": 10.0,
+           "SQ_INSTS_VALU_ADD_F64": 10.0, "SQ_INSTS_VALU_TRANS_F64": 1.0, "SQ_INSTS_VALU_INT64": 4.0,
+           "SQ_INSTS_VALU_INT32": 10.0, "SQ_INSTS_VALU_CVT": 5.0, "SQ_INSTS_VALU_ADD_F32": 0.0,
+           "SQ_INSTS_VALU_MUL_F32": 0.0, "SQ_INSTS_VALU_FMA_F32": 0.0, "SQ_INSTS_VALU_TRANS_F32": 0.0,
+           "SQ_THREAD_CYCLES_VALU": 3000.0, "SQ_ACTIVE_INST_VALU": 100.0, "GRBM_GUI_ACTIVE": 8 * 2.0e9 * 1e-6}
+    r = b.valu_roofline(pmc, 1000, 1e-6, "C2")
+    d = r["valu_detail"]
+    assert d["rest"] == 100 - 40 - 1 - 4 - 10 - 5
+    assert d["frac_lower"] < r["frac"] < d["frac_upper"]
+    assert 3.5 < d["issue_cycles_per_instr"]["rest"] < 4.5 and 2.0 < d["issue_cycles_per_instr"]["int32"] < 4.3
+    busy = 4.2 * 40 + 16.2 + 4.5 * 4 + sum(d["issue_cycles_per_instr"][k] * d[k] for k in ("int32", "cvt", "f32", "rest"))
+    assert abs(d["busy_simd_cycles"] - busy) < 1e-9
