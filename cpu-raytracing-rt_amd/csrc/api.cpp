@@ -66,7 +66,7 @@ struct rt_scene {
     // streams never overlap on the shared workspace.
     hipEvent_t ws_done = nullptr;
     // requested kernel form (rt_scene_set_tuning); auto fields resolve per scene
-    rt_tuning tune{0, -1, 0, 0, 0, 0, -1, 0};
+    rt_tuning tune{0, -1, 0, 0, 0, 0, -1, -1};
 };
 
 namespace {
@@ -240,11 +240,13 @@ int ensure_part(rt_scene* s, const KParams& k) {
 }
 
 // Spill area for stack entries beyond the LDS short stack: depth bound of the
-// deepest BVH, one slot per launched lane.
-int ensure_spill(rt_scene* s, uint64_t lanes) {
+// deepest BVH, one slot per launched lane (`no_lds`: a kernel without an LDS
+// stack, sort_kernel, spills every entry).
+int ensure_spill(rt_scene* s, uint64_t lanes, bool no_lds = false) {
     uint32_t depth = s->dev.max_depth;
-    if (depth <= (uint32_t)kMinShort) return RT_OK;
-    size_t need = (size_t)(depth - kMinShort) * lanes;
+    const uint32_t lds = no_lds ? 0u : (uint32_t)kMinShort;
+    if (depth <= lds) return RT_OK;
+    size_t need = (size_t)(depth - lds) * lanes;
     if (need <= s->spill_entries) return RT_OK;
     if (int rc = ws_idle(s)) return rc;
     if (s->spill_n) (void)hipFree(s->spill_n);
@@ -299,6 +301,16 @@ bool path_compact(const rt_scene* s) {
     return s->tune.compact != 0 && s->dev.tris.cnodes && path_waves(s) == 4 && path_resume(s) && path_kinds(s) == 2;
 }
 
+// Regrouped shading (render.hip sort_kernel): the shape-only fused kernel with
+// the shading step dealt to the waves of a 4-wave workgroup by branch class.
+// rt_tuning.sorted forces it on (1) or off (0); it applies to shape-only scenes
+// on the fused segment form only (other scenes run path_kernel).
+bool sort_eligible(const rt_scene* s) { return path_kinds(s) == 1 && !path_resume(s); }
+bool path_sorted(const rt_scene* s) {
+    if (!sort_eligible(s)) return false;
+    return s->tune.sorted >= 0 ? s->tune.sorted == 1 : kSortAuto;
+}
+
 // Suspend threshold of the resumable traversal (render.h kSuspendCached /
 // kSuspendStreamed): by whether the triangle BVH and its hot records fit the
 // Infinity Cache.  rt_tuning.suspend_lanes forces one (tuning).
@@ -335,11 +347,13 @@ int prepare_path(rt_scene* s, KParams& k, bool stats, bool hits, PathWork& W) {
     W.waves = path_waves(s);
     W.resume = path_resume(s);
     W.kinds = path_compact(s) ? kKindsCompact : path_kinds(s);
-    HIP_TRY(path_grid(stats, hits, W.waves, W.resume, W.kinds, (uint32_t)n_units, &W.grid));
+    W.sorted = path_sorted(s);
+    HIP_TRY(path_grid(stats, hits, W.waves, W.resume, W.kinds, (uint32_t)n_units, &W.grid, W.sorted));
+    const uint64_t lanes = (uint64_t)W.grid * (W.sorted ? kSortLanes : 64u);
     int rc;
-    if ((rc = ensure_spill(s, (uint64_t)W.grid * 64)) || (rc = ensure_part(s, k))) return rc;
+    if ((rc = ensure_spill(s, lanes, W.sorted)) || (rc = ensure_part(s, k))) return rc;
     if (!s->queue) HIP_TRY(hipMalloc(&s->queue, kQueueWords * sizeof(uint32_t)));
-    const size_t ring_need = (size_t)W.grid * kRingRows * 64 * 3;
+    const size_t ring_need = (size_t)W.grid * (W.sorted ? kSortRingRows : kRingRows) * 64 * 3;
     if (ring_need > s->ring_entries) {
         if (int rc2 = ws_idle(s)) return rc2;
         if (s->ring) (void)hipFree(s->ring);
@@ -593,7 +607,7 @@ int rt_scene_sample_chunks(const rt_scene* s, const rt_render_params* p, uint32_
 
 int rt_scene_set_tuning(rt_scene* s, const rt_tuning* t) {
     if (!s) return set_error(RT_ERR_INVALID, "scene is NULL");
-    if (!t) { s->tune = rt_tuning{0, -1, 0, 0, 0, 0, -1, 0}; return RT_OK; }
+    if (!t) { s->tune = rt_tuning{0, -1, 0, 0, 0, 0, -1, -1}; return RT_OK; }
     if (t->waves != 0 && t->waves != 3 && t->waves != 4) return set_error(RT_ERR_INVALID, "waves must be 0, 3 or 4");
     if (t->resume < -1 || t->resume > 1) return set_error(RT_ERR_INVALID, "resume must be -1, 0 or 1");
     if (t->kinds > 3) return set_error(RT_ERR_INVALID, "kinds must be 0..3");
@@ -604,6 +618,7 @@ int rt_scene_set_tuning(rt_scene* s, const rt_tuning* t) {
     if (t->compact < -1 || t->compact > 1) return set_error(RT_ERR_INVALID, "compact must be -1, 0 or 1");
     if (t->compact == 1 && !s->dev.tris.cnodes)
         return set_error(RT_ERR_UNSUPPORTED, "compact = 1: the scene has no compact triangle layout");
+    if (t->sorted < -1 || t->sorted > 1) return set_error(RT_ERR_INVALID, "sorted must be -1, 0 or 1");
     s->tune = *t;
     return RT_OK;
 }
@@ -617,7 +632,7 @@ int rt_scene_get_tuning(const rt_scene* s, rt_tuning* out) {
     out->leaf_lanes = path_leaf_batch(s);
     out->chunk_spp = s->tune.chunk_spp;
     out->compact = path_compact(s) ? 1 : 0;
-    out->_reserved = 0;
+    out->sorted = path_sorted(s) ? 1 : 0;
     return RT_OK;
 }
 

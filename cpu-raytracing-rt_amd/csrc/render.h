@@ -81,9 +81,14 @@ struct PathWork {
     uint32_t* queue;      // wave-tile counter, zeroed by launch_path
     double* ring;         // [grid][kRing=8][64][3] finished-path radiance
     double* part;         // [n_slots*chunks][256][3] chunk partial sums (chunks > 1)
-    uint32_t* spill_n;    // traversal-stack spill, stride grid*64
+    uint32_t* spill_n;    // traversal-stack spill, stride grid*64 (grid*kSortLanes when sorted)
     double* spill_t;
+    bool sorted;          // the regrouped-shading kernel (render.hip sort_kernel): shape-only fused scenes
 };
+// sort_kernel: workgroups of kSortLanes path slots, a commit window of kSortRingRows
+// rows per workgroup, no LDS stack (spill sized for the whole BVH depth)
+constexpr uint32_t kSortLanes = 256, kSortRingRows = 16;
+constexpr bool kSortAuto = false;  // the host's pick for eligible scenes (api.cpp path_sorted)
 #ifndef RT_RING_ROWS
 #define RT_RING_ROWS 8
 #endif
@@ -107,7 +112,7 @@ constexpr uint64_t kDeepSceneNodes = 4096;  // BVH nodes above which the 4-wave 
 constexpr size_t kQueueWords = 16;  // wave-tile counter (word 0), padded to a 64-B line
 
 hipError_t path_grid(bool stats, bool hits, uint32_t waves, bool resume, int kinds, uint32_t n_units,
-                     uint32_t* grid);
+                     uint32_t* grid, bool sorted = false);
 hipError_t launch_path(const DevScene& S, const KParams& P, const PathWork& W, double* out, int32_t* hit_ids,
                        unsigned long long* stats, hipStream_t st);
 hipError_t launch_reduce_chunks(const double* part, double* out, const KParams& P, hipStream_t st);

@@ -317,17 +317,39 @@ void build_compact(const HostBvh& h, const std::vector<TriItem>& items, HostBvhA
         if (!f32_exact3(n.box.min) || !f32_exact3(n.box.max)) return;
     for (const TriItem& it : items)
         if (!f32_exact3(it.t.a) || !f32_exact3(it.b) || !f32_exact3(it.c)) return;
-    // Record slots: pre-order (the reference's numbering, bvh.rs:104), so a node and
-    // its left child share a 128-B line half the time.  (Pairing siblings in one line
-    // was measured neutral in round 3.)
-    std::vector<uint32_t> slot(h.nodes.size());
-    size_t n_slots = h.nodes.size();
-    for (size_t i = 0; i < h.nodes.size(); ++i) slot[i] = (uint32_t)i;
+    // Record slots (round 4): the INTERNAL nodes only, in pre-order (the reference's
+    // numbering, bvh.rs:104, with the leaves left out), then the leaves a child word
+    // cannot pack (child_word: kLeafRef, >= 128 primitives or a start past 2^24).  A
+    // packed leaf is entered from its parent's word and never read as a node, so its
+    // 64-B entry was dead weight between the internal nodes: without it the array
+    // halves (C5: the internal nodes of a 10M-triangle tree come near the 256-MiB
+    // Infinity Cache) and an internal node's internal left child is the next slot,
+    // the other half of its 128-B line as often as the node sits at an even slot.
+    // Only the addresses change: every lane's visits and tests are the same.
+    auto packs = [](const HostNode& n) {
+        const uint64_t cnt = n.end - n.start;
+        return cnt < 128u && n.start < (1u << 24);
+    };
+    const uint32_t kNone = ~0u;
+    std::vector<uint32_t> slot(h.nodes.size(), kNone);
+    size_t n_slots = 0;
+    for (size_t i = 0; i < h.nodes.size(); ++i)  // h.nodes is in pre-order
+        if (h.nodes[i].left >= 0) slot[i] = (uint32_t)n_slots++;
+    if (n_slots == 0 || slot[0] != 0) return;  // a leaf root: nothing to traverse
+    for (size_t i = 0; i < h.nodes.size(); ++i)
+        if (h.nodes[i].left < 0 && !packs(h.nodes[i])) slot[i] = (uint32_t)n_slots++;
     if (n_slots >= kLeafRef) return;
     std::vector<DevNodeC> cn(n_slots);
     std::memset(cn.data(), 0, n_slots * sizeof(DevNodeC));
     auto put3 = [](float* d, V3 v) { d[0] = (float)v.x; d[1] = (float)v.y; d[2] = (float)v.z; };
+    auto word = [&](const HostNode& c, int64_t idx) {
+        const uint32_t cnt = (uint32_t)(c.end - c.start);
+        if (c.left >= 0) return slot[idx];                                       // internal
+        if (packs(c)) return kPackedLeaf | (cnt << 24) | (uint32_t)c.start;       // packed leaf
+        return slot[idx] | kLeafRef;                                             // big leaf entry
+    };
     for (size_t i = 0; i < h.nodes.size(); ++i) {
+        if (slot[i] == kNone) continue;
         const HostNode& n = h.nodes[i];
         DevNodeC c;
         std::memset(&c, 0, sizeof(c));
@@ -336,8 +358,8 @@ void build_compact(const HostBvh& h, const std::vector<TriItem>& items, HostBvhA
             const HostNode& r = h.nodes[n.right];
             put3(c.lmin, l.box.min); put3(c.lmax, l.box.max);
             put3(c.rmin, r.box.min); put3(c.rmax, r.box.max);
-            c.lw = child_word(slot[n.left], (uint32_t)l.start, (uint32_t)(l.end - l.start));
-            c.rw = child_word(slot[n.right], (uint32_t)r.start, (uint32_t)(r.end - r.start));
+            c.lw = word(l, n.left);
+            c.rw = word(r, n.right);
         }
         c.start = (uint32_t)n.start;
         c.count = (uint32_t)(n.end - n.start);

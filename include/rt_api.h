@@ -213,7 +213,9 @@ typedef struct rt_tuning {
     int32_t  compact;        /* -1 auto (1 when the scene has it: RT_LAYOUT_COMPACT_TRIS); 0 the f64
                                 triangle-BVH layout; 1 the compact one (triangle-only resumable kernel;
                                 RT_ERR_UNSUPPORTED on a scene without RT_LAYOUT_COMPACT_TRIS)           */
-    uint32_t _reserved;
+    int32_t  sorted;         /* -1 auto; 1 the regrouped-shading kernel (shading dealt to the waves of a
+                                4-wave workgroup by branch class) for shape-only
+                                scenes on the fused segment form; 0 the one-wave kernel             */
 } rt_tuning;
 /* NULL restores every field to auto.  Fields out of range -> RT_ERR_INVALID. */
 int rt_scene_set_tuning(rt_scene* scene, const rt_tuning* tuning);

@@ -34,7 +34,7 @@ def sink(rt, orc, scene_text):
 FORM = {}
 
 
-@pytest.fixture(autouse=True, params=["fused", "resume", "resume_eager", "resume_f64", "general"])
+@pytest.fixture(autouse=True, params=["fused", "resume", "resume_eager", "resume_f64", "general", "sorted"])
 def segment_form(request):
     """Every test runs both path-kernel segment forms: fused (whole closest-hit
     query, then shading) and resumable (triangle traversal suspended while few
@@ -46,7 +46,10 @@ def segment_form(request):
     host would pick a shape-only or triangle-only one (api.cpp path_kinds).
     The resumable forms read a glTF scene's triangle BVH in its compact layout
     (f32 child boxes and vertices, exact copies: api.cpp path_compact);
-    "resume_f64" forces the f64 layout in the same kernel."""
+    "resume_f64" forces the f64 layout in the same kernel.
+    "sorted" runs shape-only scenes through the regrouped-shading kernel (render.hip
+    sort_kernel: paths in LDS slots of a 4-wave workgroup, shading dealt to the waves
+    by branch class); other scenes keep the fused one-wave kernel."""
     FORM.clear()
     FORM["resume"] = 1 if request.param.startswith("resume") else 0
     if request.param == "resume_eager":
@@ -55,6 +58,7 @@ def segment_form(request):
         FORM["compact"] = 0
     if request.param == "general":
         FORM["kinds"] = 3
+    FORM["sorted"] = 1 if request.param == "sorted" else 0
     yield request.param
     FORM.clear()
 
@@ -156,9 +160,18 @@ def test_dev_sqrt_matches_host(rt):
     assert np.isnan(got_i[~ok]).all()
 
 
-def test_cornell_small(cornell):
+def test_cornell_small(cornell, segment_form):
     desc, params, g, o = cornell
     _compare(g, o, params.replace(width=48, height=40, spp=4))
+    # shape-only on the fused form: the sorted form runs the regrouped kernel
+    assert g.tuning()["sorted"] == (1 if segment_form == "sorted" else 0)
+
+
+def test_sorted_wide_frame(cornell, segment_form):
+    """A frame with many wave-tiles per workgroup and long paths: the regrouped kernel's
+    workgroup stream (rows dealt to 256 slots, the 16-row commit window) in every form."""
+    desc, params, g, o = cornell
+    _compare(g, o, params.replace(width=96, height=64, spp=9, ray_depth=20, seed=5))
 
 
 @pytest.mark.parametrize("waves", [3, 4])

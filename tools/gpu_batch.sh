@@ -107,6 +107,11 @@ for s in $STEPS; do
              --timeout-method thread || exit 1 ;;
     kids)  run kid_stats 600 python3 tools/kid_stats.py C3 64 C5 16 || exit 1 ;;
     valu)  run valu_rates 300 tools/valu_rates full || exit 1 ;;
+    lanes2|lanes3)  # active lanes per VALU instruction of a variant library ($LANES_LIB, default the product)
+      w=C${s#lanes}
+      RT_AMD_LIB=${LANES_LIB:-$PWD/cpu-raytracing-rt_amd/build/librt_amd.so} run lanes_$w 600 rocprofv3 --pmc \
+        SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVE_CYCLES --output-format csv -d "$OUT/lanes_$w" \
+        -o run -- $B --workload $w --steps 1 --warmup 0 --no-cpu-baseline --no-pmc --spp ${LANES_SPP:-64} || exit 1 ;;
     *)     echo "unknown step $s"; exit 2 ;;
   esac
 done
