@@ -353,8 +353,32 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
         PH_COUNT(kPhInnerWave, kPhInnerLane);
         double lt = 0.0, rt2 = 0.0;
         C.aabb(2);
+#ifdef RT_EXP_PREFILTER
+        // Experiment (round 4): an f32 certain-miss prefilter.  With |o|, |r| < 2^100 the
+        // f32 slab quotient of a plane is within e = (|lo| + |hi| + 2|o|)|r| 2^-20 of the
+        // exact one, so max(near - e) > min(far + e), or min(far + e) < 0, proves a miss of
+        // the f64 test; such a child skips its f64 slab (exec-masked: the wave still runs
+        // it for the other lanes).  Same visits and results.
+        const bool pf = fabs(o.x) < 0x1p100 && fabs(o.y) < 0x1p100 && fabs(o.z) < 0x1p100 &&
+                        fabs(rc.r.x) < 0x1p100 && fabs(rc.r.y) < 0x1p100 && fabs(rc.r.z) < 0x1p100;
+        const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
+        const float rx = (float)rc.r.x, ry = (float)rc.r.y, rz = (float)rc.r.z;
+        auto miss32 = [&](float lx, float ly, float lz, float hx, float hy, float hz) {
+            const float ax = (lx - ox) * rx, bx = (hx - ox) * rx, ex = (fabsf(lx) + fabsf(hx) + 2.0f * fabsf(ox)) * fabsf(rx) * 0x1p-20f;
+            const float ay = (ly - oy) * ry, by = (hy - oy) * ry, ey = (fabsf(ly) + fabsf(hy) + 2.0f * fabsf(oy)) * fabsf(ry) * 0x1p-20f;
+            const float az = (lz - oz) * rz, bz = (hz - oz) * rz, ez = (fabsf(lz) + fabsf(hz) + 2.0f * fabsf(oz)) * fabsf(rz) * 0x1p-20f;
+            const float tn = fmaxf(fmaxf(fminf(ax, bx) - ex, fminf(ay, by) - ey), fminf(az, bz) - ez);
+            const float tf = fminf(fminf(fmaxf(ax, bx) + ex, fmaxf(ay, by) + ey), fmaxf(az, bz) + ez);
+            return pf && (tn > tf || tf < 0.0f);
+        };
+        const bool lm = miss32(w0.x, w0.y, w0.z, w0.w, w1.x, w1.y);
+        const bool rm = miss32(w1.z, w1.w, w2.x, w2.y, w2.z, w2.w);
+        const bool lh = !lm && slab_c<SLAB>(w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, o, d, rc, fast, lt);
+        const bool rh = !rm && slab_c<SLAB>(w1.z, w1.w, w2.x, w2.y, w2.z, w2.w, o, d, rc, fast, rt2);
+#else
         const bool lh = slab_c<SLAB>(w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, o, d, rc, fast, lt);
         const bool rh = slab_c<SLAB>(w1.z, w1.w, w2.x, w2.y, w2.z, w2.w, o, d, rc, fast, rt2);
+#endif
         C.kids(lh, rh);
         const double bt = T.best;  // +inf when no hit yet
         const double li = lh ? (lt < bt ? lt : bt) : bt;

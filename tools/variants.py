@@ -22,13 +22,15 @@ if depth:
 s = rt.Scene(desc)
 tune = {k: int(v) for k, v in (kv.split("=", 1) for kv in os.environ.get("RT_VARIANT_ENV", "").split(",") if kv)}
 s.set_tuning(**tune)
+import hashlib
 _, _, st = s.generate_image(params, stats=True)
 ks = []
 for i in range(3):
-    _, _, st2 = s.generate_image(params)
+    img, _, st2 = s.generate_image(params)
     ks.append(st2["kernel_ms"])
 print(json.dumps({"lib": os.environ["RT_AMD_LIB"], "tuning": s.tuning(), "workload": sys.argv[2], "spp": params.spp, "kernel_ms": ks,
-                  "Mseg_s": st["segments"] / min(ks) / 1e3, "segments": st["segments"]}))
+                  "Mseg_s": st["segments"] / min(ks) / 1e3, "segments": st["segments"],
+                  "image_sha256": hashlib.sha256(img.tobytes()).hexdigest()[:16]}))
 '''
 wl, spp = sys.argv[1], sys.argv[2]
 rc = 0
