@@ -152,6 +152,7 @@ def pmc_counters(args, world):
             cmd = ["rocprofv3", "--pmc", *counters, "--output-format", "csv", "-d", d, "-o", "run", "--",
                    sys.executable, os.path.abspath(__file__), "--workload", args.workload, "--steps", "1",
                    "--warmup", "0", "--no-cpu-baseline", "--no-pmc", "--as-rank0-of", str(world)]
+            cmd += ["--tune", args.tune] if args.tune else []
             cmd += ["--spp", str(args.spp)] if args.spp else []
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env)
             if r.returncode != 0:
@@ -322,6 +323,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc child passes (roofline=null)")
     ap.add_argument("--as-rank0-of", type=int, default=0, help=argparse.SUPPRESS)  # PMC child: rank 0's share
+    ap.add_argument("--tune", default="", help="experiments: force rt_tuning fields, e.g. sorted=1,waves=4 "
+                                                  "(the headline runs the library's own pick)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (RCCL over xGMI, the product path); gloo gathers host copies and lets several "
                          "ranks share one GPU (a rehearsal of the N>1 path on a one-GPU box)")
@@ -358,6 +361,8 @@ def main():
     t0 = time.perf_counter()
     scene = rt.Scene(desc)
     build_s = time.perf_counter() - t0
+    if args.tune:
+        scene.set_tuning(**{k: int(v) for k, v in (kv.split("=", 1) for kv in args.tune.split(","))})
 
     # a PMC child renders rank 0's tile share of the parent's partition, alone
     part = args.as_rank0_of or world

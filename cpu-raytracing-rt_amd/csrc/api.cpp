@@ -65,6 +65,8 @@ struct rt_scene {
     // stream wait on it, then re-records it, so calls issued on different
     // streams never overlap on the shared workspace.
     hipEvent_t ws_done = nullptr;
+    // bytes of the triangle BVH's compact layout (nodes + leaf blocks), 0 without one
+    uint64_t compact_bytes = 0;
     // requested kernel form (rt_scene_set_tuning); auto fields resolve per scene
     rt_tuning tune{0, -1, 0, 0, 0, 0, -1, -1};
 };
@@ -318,9 +320,8 @@ bool path_sorted(const rt_scene* s) {
 // layout the kernel reads (path_compact: 64-B nodes and 36-B records, else 128 B
 // and 80 B).
 uint64_t bvh_hot_bytes(const rt_scene* s) {
-    const bool cmp = path_compact(s);
-    return s->info.bvh_nodes[2] * (cmp ? sizeof(DevNodeC) : sizeof(DevNode)) +
-           s->info.n_triangles * (cmp ? kTriC * sizeof(float) : sizeof(DevTri));
+    if (path_compact(s)) return s->compact_bytes;
+    return s->info.bvh_nodes[2] * sizeof(DevNode) + s->info.n_triangles * sizeof(DevTri);
 }
 bool bvh_streamed(const rt_scene* s) { return bvh_hot_bytes(s) > kCacheBytes; }
 uint32_t path_suspend(const rt_scene* s) {
@@ -562,6 +563,7 @@ int scene_upload(const HostScene& hs, rt_scene** out) {
     s->info.n_light_ellipsoids = d.lells.n_prims;
     s->info.n_light_triangles = d.ltris.n_prims;
     s->info.shared_light_mask = d.slt_mask;
+    s->compact_bytes = hs.bvh[2].cnodes.size() * sizeof(DevNodeC) + hs.bvh[2].ctris.size() * sizeof(float);
     s->info.layout_flags = (d.tris.cnodes ? RT_LAYOUT_COMPACT_TRIS : 0u) | (d.lq_boxes ? RT_LAYOUT_LQ_SKIP : 0u);
     s->info.build_ms = hs.build_ms;
     s->info.upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

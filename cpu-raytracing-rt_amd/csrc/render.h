@@ -87,7 +87,10 @@ struct PathWork {
 };
 // sort_kernel: workgroups of kSortLanes path slots, a commit window of kSortRingRows
 // rows per workgroup, no LDS stack (spill sized for the whole BVH depth)
-constexpr uint32_t kSortLanes = 256, kSortRingRows = 16;
+#ifndef RT_SORT_WAVES
+#define RT_SORT_WAVES 4
+#endif
+constexpr uint32_t kSortLanes = 64 * RT_SORT_WAVES, kSortRingRows = 16;
 constexpr bool kSortAuto = false;  // the host's pick for eligible scenes (api.cpp path_sorted)
 #ifndef RT_RING_ROWS
 #define RT_RING_ROWS 8

@@ -300,14 +300,18 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
                     // kernel pays in spills (a traversal-only kernel needs 105 VGPRs with it,
                     // 84 without): C3 -0.9%, C5 -1.9% at reduced spp
                     // (profiles/r03/variants/variants_leafpipe_C*.log).
-                    for (uint32_t i = T.start; i < end; ++i) {
+                    // the leaf's block (rt_layout.h kLeafBlock): T.start is its index, the
+                    // first word its first primitive, then the records in order
+                    const float* blk = B.ctris + (size_t)T.start * kLeafBlock;
+                    const uint32_t first = *(const uint32_t*)blk;
+                    for (uint32_t k = 0; k < T.cnt; ++k) {
                         PH_COUNT(kPhLeafWave, kPhLeafLane);
-                        const TriRec cur = load_tri_c(B.ctris + (size_t)i * kTriC);
+                        const TriRec cur = load_tri_c(blk + 1 + k * kTriC);
                         double t, u = 0.0, v = 0.0;
                         C.tri();
                         const bool h = tri_uvt_r(cur, o, d, u, v, t);
                         if (h && (!T.valid || t < T.best)) {  // update_best_intersection (bvh.rs:213-222)
-                            T.valid = true; T.best = t; T.prim = i; T.aux = 0;
+                            T.valid = true; T.best = t; T.prim = first + k; T.aux = 0;
                             T.bu = u; T.bv = v;
                         }
                     }
@@ -353,32 +357,8 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
         PH_COUNT(kPhInnerWave, kPhInnerLane);
         double lt = 0.0, rt2 = 0.0;
         C.aabb(2);
-#ifdef RT_EXP_PREFILTER
-        // Experiment (round 4): an f32 certain-miss prefilter.  With |o|, |r| < 2^100 the
-        // f32 slab quotient of a plane is within e = (|lo| + |hi| + 2|o|)|r| 2^-20 of the
-        // exact one, so max(near - e) > min(far + e), or min(far + e) < 0, proves a miss of
-        // the f64 test; such a child skips its f64 slab (exec-masked: the wave still runs
-        // it for the other lanes).  Same visits and results.
-        const bool pf = fabs(o.x) < 0x1p100 && fabs(o.y) < 0x1p100 && fabs(o.z) < 0x1p100 &&
-                        fabs(rc.r.x) < 0x1p100 && fabs(rc.r.y) < 0x1p100 && fabs(rc.r.z) < 0x1p100;
-        const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
-        const float rx = (float)rc.r.x, ry = (float)rc.r.y, rz = (float)rc.r.z;
-        auto miss32 = [&](float lx, float ly, float lz, float hx, float hy, float hz) {
-            const float ax = (lx - ox) * rx, bx = (hx - ox) * rx, ex = (fabsf(lx) + fabsf(hx) + 2.0f * fabsf(ox)) * fabsf(rx) * 0x1p-20f;
-            const float ay = (ly - oy) * ry, by = (hy - oy) * ry, ey = (fabsf(ly) + fabsf(hy) + 2.0f * fabsf(oy)) * fabsf(ry) * 0x1p-20f;
-            const float az = (lz - oz) * rz, bz = (hz - oz) * rz, ez = (fabsf(lz) + fabsf(hz) + 2.0f * fabsf(oz)) * fabsf(rz) * 0x1p-20f;
-            const float tn = fmaxf(fmaxf(fminf(ax, bx) - ex, fminf(ay, by) - ey), fminf(az, bz) - ez);
-            const float tf = fminf(fminf(fmaxf(ax, bx) + ex, fmaxf(ay, by) + ey), fmaxf(az, bz) + ez);
-            return pf && (tn > tf || tf < 0.0f);
-        };
-        const bool lm = miss32(w0.x, w0.y, w0.z, w0.w, w1.x, w1.y);
-        const bool rm = miss32(w1.z, w1.w, w2.x, w2.y, w2.z, w2.w);
-        const bool lh = !lm && slab_c<SLAB>(w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, o, d, rc, fast, lt);
-        const bool rh = !rm && slab_c<SLAB>(w1.z, w1.w, w2.x, w2.y, w2.z, w2.w, o, d, rc, fast, rt2);
-#else
         const bool lh = slab_c<SLAB>(w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, o, d, rc, fast, lt);
         const bool rh = slab_c<SLAB>(w1.z, w1.w, w2.x, w2.y, w2.z, w2.w, o, d, rc, fast, rt2);
-#endif
         C.kids(lh, rh);
         const double bt = T.best;  // +inf when no hit yet
         const double li = lh ? (lt < bt ? lt : bt) : bt;
@@ -1162,14 +1142,7 @@ RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, P
     rng_align(rng);   // shading draws start on a block boundary (oracle.c rng_align)
     rng_top_up(rng);  // every hit lane here: a coherent refill point
     const V3 o = ps.o, d = ps.d;
-#if defined(RT_EXP_BOUND) && RT_EXP_BOUND & 1
-    // Experiment (not the reference's estimator): the shading step without its
-    // divergence — every material shaded as diffuse (bit 0) and one Mix coin per wave
-    // (bit 1) — the bound on what regrouping lanes by branch class could save
-    if (true) {
-#else
     if (m.kind == RT_MAT_DIFFUSE) {  // :16-34
-#endif
         V3 pos = o + d * h.t;
         const bool empty = S.n_lights == 0;
         V3 dir;
@@ -1178,9 +1151,6 @@ RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, P
         bool by_cosine;
         uint64_t ua, ub, uc;
         diffuse_draws(rng, !empty, by_cosine, ua, ub, uc);
-#if defined(RT_EXP_BOUND) && RT_EXP_BOUND & 2
-        by_cosine = __builtin_amdgcn_readfirstlane(by_cosine ? 1u : 0u) != 0u;
-#endif
         // both samplers end in normalize(w): one call after the branches join
         V3 sw;
         bool degen = false;
@@ -1707,7 +1677,7 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
 //   E  wave 0 commits finished rows in sample order (as path_kernel).
 // Each path's arithmetic and RNG words are path_kernel's: bit-identical images,
 // hit ids and counters (the parity suite's "sorted" form).
-constexpr int kSortW = 4;                  // waves per workgroup
+constexpr int kSortW = RT_SORT_WAVES;      // waves per workgroup (render.h)
 constexpr int kSortN = kSortW * kWave;     // path slots per workgroup
 constexpr int kSortRing = 16;              // rows of the commit window (256 paths in flight)
 static_assert(kSortN == (int)kSortLanes && kSortRing == (int)kSortRingRows, "render.h sort_kernel constants");
@@ -1769,7 +1739,9 @@ __global__ __launch_bounds__(kSortN, 3) void sort_kernel(const DevScene* __restr
         const uint64_t im = __ballot(idle);
         if (lane == 0) s_idle[wv] = (uint32_t)__popcll(im);
         __syncthreads();
-        const uint32_t n_idle = s_idle[0] + s_idle[1] + s_idle[2] + s_idle[3];
+        uint32_t n_idle = 0;
+#pragma unroll
+        for (int w = 0; w < kSortW; ++w) n_idle += s_idle[w];
         uint32_t before = 0;
         for (uint32_t w = 0; w < wv; ++w) before += s_idle[w];
         const uint32_t window = (g.base + kSortRing) * kWave;
@@ -1925,6 +1897,9 @@ __global__ __launch_bounds__(kSortN, 3) void sort_kernel(const DevScene* __restr
         }
         ++witers;
         if (tid == 0) g.next = min(limit, next + n_idle);
+        // the ring stores of this trip have reached the L2 before wave 0 reads them (past
+        // its L1) in the commit below
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         // ---- E: commit complete rows in stream order (wave 0: one lane per pixel of
         // the wave-tile's 8x8 quadrant); the last row of the oldest open wave-tile writes

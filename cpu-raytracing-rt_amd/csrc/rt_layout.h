@@ -68,6 +68,10 @@ static_assert(sizeof(DevNodeC) == 64, "compact node is half a line");
 // device rebuilds ba = b - a, ca = c - a in f64 — the same bits as the host's,
 // which triangle_props computed from the same a, b, c).
 constexpr uint32_t kTriC = 9;   // floats per compact triangle record
+// Compact records are stored in leaf blocks (round 4, scene_build.cpp build_compact): a
+// leaf's records behind a one-word header (its first primitive index), the block on a
+// 128-B line; a leaf's child word / big-leaf entry carries the block index.
+constexpr uint32_t kLeafBlock = 32;  // floats per 128-B line
 
 struct alignas(16) DevShape {  // Primitive<T> hot part (scene.rs:20-27)
     double shape[3];           // plane normal | box half sizes | ellipsoid radii

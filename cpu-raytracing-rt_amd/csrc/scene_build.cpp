@@ -317,18 +317,34 @@ void build_compact(const HostBvh& h, const std::vector<TriItem>& items, HostBvhA
         if (!f32_exact3(n.box.min) || !f32_exact3(n.box.max)) return;
     for (const TriItem& it : items)
         if (!f32_exact3(it.t.a) || !f32_exact3(it.b) || !f32_exact3(it.c)) return;
+    // Triangle records in LEAF BLOCKS (round 4): each leaf's records, a, b, c as f32
+    // (kTriC floats), contiguous behind a one-word header holding the leaf's first
+    // primitive index, the block starting on a 128-B line (kLeafBlock floats).  A leaf of
+    // up to three triangles is one line (112 B), four are two; unaligned 36-B records
+    // spread a leaf over 1.3-2.1 lines (profiles/r03/fetch_calib.log: a random 36-B
+    // record costs 4.4x its bytes in 128-B lines).  The leaf's child word carries the
+    // block index instead of the first primitive.
+    std::vector<uint64_t> block(h.nodes.size(), 0);
+    uint64_t n_floats = 0;
+    for (size_t i = 0; i < h.nodes.size(); ++i) {
+        const HostNode& n = h.nodes[i];
+        if (n.left >= 0) continue;
+        block[i] = n_floats / kLeafBlock;
+        const uint64_t len = 1 + (uint64_t)kTriC * (n.end - n.start);
+        n_floats += (len + kLeafBlock - 1) / kLeafBlock * kLeafBlock;
+    }
     // Record slots (round 4): the INTERNAL nodes only, in pre-order (the reference's
     // numbering, bvh.rs:104, with the leaves left out), then the leaves a child word
-    // cannot pack (child_word: kLeafRef, >= 128 primitives or a start past 2^24).  A
-    // packed leaf is entered from its parent's word and never read as a node, so its
-    // 64-B entry was dead weight between the internal nodes: without it the array
-    // halves (C5: the internal nodes of a 10M-triangle tree come near the 256-MiB
-    // Infinity Cache) and an internal node's internal left child is the next slot,
-    // the other half of its 128-B line as often as the node sits at an even slot.
-    // Only the addresses change: every lane's visits and tests are the same.
-    auto packs = [](const HostNode& n) {
-        const uint64_t cnt = n.end - n.start;
-        return cnt < 128u && n.start < (1u << 24);
+    // cannot pack (kLeafRef: >= 128 primitives or a block index past 2^24).  A packed
+    // leaf is entered from its parent's word and never read as a node, so its 64-B
+    // entry was dead weight between the internal nodes: without it the array halves
+    // (C5: the internal nodes of a 10M-triangle tree come near the 256-MiB Infinity
+    // Cache) and an internal node's internal left child is the next slot, the other
+    // half of its 128-B line as often as the node sits at an even slot.  Only the
+    // addresses change: every lane's visits and tests are the same.
+    auto packs = [&](size_t idx) {
+        const HostNode& n = h.nodes[idx];
+        return n.end - n.start < 128u && block[idx] < (1u << 24);
     };
     const uint32_t kNone = ~0u;
     std::vector<uint32_t> slot(h.nodes.size(), kNone);
@@ -337,16 +353,17 @@ void build_compact(const HostBvh& h, const std::vector<TriItem>& items, HostBvhA
         if (h.nodes[i].left >= 0) slot[i] = (uint32_t)n_slots++;
     if (n_slots == 0 || slot[0] != 0) return;  // a leaf root: nothing to traverse
     for (size_t i = 0; i < h.nodes.size(); ++i)
-        if (h.nodes[i].left < 0 && !packs(h.nodes[i])) slot[i] = (uint32_t)n_slots++;
-    if (n_slots >= kLeafRef) return;
+        if (h.nodes[i].left < 0 && !packs(i)) slot[i] = (uint32_t)n_slots++;
+    if (n_slots >= kLeafRef || n_floats / kLeafBlock >= (1ull << 32)) return;
     std::vector<DevNodeC> cn(n_slots);
     std::memset(cn.data(), 0, n_slots * sizeof(DevNodeC));
     auto put3 = [](float* d, V3 v) { d[0] = (float)v.x; d[1] = (float)v.y; d[2] = (float)v.z; };
-    auto word = [&](const HostNode& c, int64_t idx) {
+    auto word = [&](int64_t idx) {
+        const HostNode& c = h.nodes[idx];
         const uint32_t cnt = (uint32_t)(c.end - c.start);
-        if (c.left >= 0) return slot[idx];                                       // internal
-        if (packs(c)) return kPackedLeaf | (cnt << 24) | (uint32_t)c.start;       // packed leaf
-        return slot[idx] | kLeafRef;                                             // big leaf entry
+        if (c.left >= 0) return slot[idx];                                        // internal
+        if (packs(idx)) return kPackedLeaf | (cnt << 24) | (uint32_t)block[idx];  // packed leaf block
+        return slot[idx] | kLeafRef;                                              // big leaf entry
     };
     for (size_t i = 0; i < h.nodes.size(); ++i) {
         if (slot[i] == kNone) continue;
@@ -358,17 +375,26 @@ void build_compact(const HostBvh& h, const std::vector<TriItem>& items, HostBvhA
             const HostNode& r = h.nodes[n.right];
             put3(c.lmin, l.box.min); put3(c.lmax, l.box.max);
             put3(c.rmin, r.box.min); put3(c.rmax, r.box.max);
-            c.lw = word(l, n.left);
-            c.rw = word(r, n.right);
+            c.lw = word(n.left);
+            c.rw = word(n.right);
+        } else {
+            c.start = (uint32_t)block[i];  // a big leaf: its block
         }
-        c.start = (uint32_t)n.start;
         c.count = (uint32_t)(n.end - n.start);
         cn[slot[i]] = c;
     }
-    std::vector<float> ct(items.size() * kTriC);
-    for (size_t k = 0; k < h.order.size(); ++k) {
-        const TriItem& it = items[h.order[k]];
-        put3(&ct[k * kTriC], it.t.a); put3(&ct[k * kTriC + 3], it.b); put3(&ct[k * kTriC + 6], it.c);
+    std::vector<float> ct(n_floats, 0.0f);
+    for (size_t i = 0; i < h.nodes.size(); ++i) {
+        const HostNode& n = h.nodes[i];
+        if (n.left >= 0) continue;
+        float* b = &ct[block[i] * kLeafBlock];
+        const uint32_t first = (uint32_t)n.start;
+        std::memcpy(b, &first, sizeof(first));
+        for (uint64_t k = n.start; k < n.end; ++k) {
+            const TriItem& it = items[h.order[k]];
+            float* r = b + 1 + (k - n.start) * kTriC;
+            put3(r, it.t.a); put3(r + 3, it.b); put3(r + 6, it.c);
+        }
     }
     out.cnodes = std::move(cn);
     out.ctris = std::move(ct);

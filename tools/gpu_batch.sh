@@ -112,6 +112,15 @@ for s in $STEPS; do
       RT_AMD_LIB=${LANES_LIB:-$PWD/cpu-raytracing-rt_amd/build/librt_amd.so} run lanes_$w 600 rocprofv3 --pmc \
         SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVE_CYCLES --output-format csv -d "$OUT/lanes_$w" \
         -o run -- $B --workload $w --steps 1 --warmup 0 --no-cpu-baseline --no-pmc --spp ${LANES_SPP:-64} || exit 1 ;;
+    sortpmc)  # the one-wave and the regrouped C2 kernels side by side: instruction mix, lanes, waits, LDS
+      for tn in sorted=0 sorted=1; do
+        run sq_$tn 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_VALU \
+          SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES --output-format csv -d "$OUT/sq_$tn" -o run \
+          -- $B --workload C2 --steps 1 --warmup 0 --no-cpu-baseline --no-pmc --spp 64 --tune $tn || exit 1
+        run lds_$tn 600 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_WAIT_INST_ANY \
+          SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM --output-format csv -d "$OUT/lds_$tn" -o run \
+          -- $B --workload C2 --steps 1 --warmup 0 --no-cpu-baseline --no-pmc --spp 64 --tune $tn || exit 1
+      done ;;
     *)     echo "unknown step $s"; exit 2 ;;
   esac
 done
