@@ -95,6 +95,7 @@ int upload_bvh(rt_scene* s, const HostBvhArrays& h, DevBvh& d) {
     d.n_prims = h.n_prims;
     d.depth = h.depth;
     d.fast = h.fast ? 1u : 0u;
+    d.tri_q = h.tri_q ? 1u : 0u;
     if ((rc = upload(s, h.shapes, &d.shapes))) return rc;
     if ((rc = upload(s, h.tris, &d.tris))) return rc;
     if ((rc = upload(s, h.tri_cold, &d.tri_cold))) return rc;
@@ -868,11 +869,11 @@ int rt_bvh_build(const double* boxes, uint64_t n, uint64_t* n_nodes, int64_t* ou
 }
 
 // Diagnostic: device f64 sqrt (op 0), division (op 1), the split division
-// dev_quot(a, b, dev_rcp(b)) (op 2), dev_sqrt(a) (op 3) and dev_inv_len(a)
-// (op 4) for bit-exactness checks.
+// dev_quot(a, b, dev_rcp(b)) (op 2), dev_sqrt(a) (op 3), dev_inv_len(a)
+// (op 4) and dev_quotf(a, b, dev_rcp(b)) (op 5) for bit-exactness checks.
 int rt_probe_fp64(int op, const double* a, const double* b, uint32_t n, double* out) {
-    const bool two = op == 1 || op == 2;
-    if (!a || !out || (two && !b) || op < 0 || op > 4) return set_error(RT_ERR_INVALID, "bad arguments");
+    const bool two = op == 1 || op == 2 || op == 5;
+    if (!a || !out || (two && !b) || op < 0 || op > 5) return set_error(RT_ERR_INVALID, "bad arguments");
     if (n == 0) return RT_OK;
     DevBuf<double> da, db, dout;
     HIP_TRY(da.alloc(n));

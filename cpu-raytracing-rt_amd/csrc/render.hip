@@ -304,12 +304,13 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
                     // first word its first primitive, then the records in order
                     const float* blk = B.ctris + (size_t)T.start * kLeafBlock;
                     const uint32_t first = *(const uint32_t*)blk;
+                    const bool q = dir_tq(d);
                     for (uint32_t k = 0; k < T.cnt; ++k) {
                         PH_COUNT(kPhLeafWave, kPhLeafLane);
                         const TriRec cur = load_tri_c(blk + 1 + k * kTriC);
                         double t, u = 0.0, v = 0.0;
                         C.tri();
-                        const bool h = tri_uvt_r(cur, o, d, u, v, t);
+                        const bool h = tri_uvt_r<true>(cur, o, d, u, v, t, q);
                         if (h && (!T.valid || t < T.best)) {  // update_best_intersection (bvh.rs:213-222)
                             T.valid = true; T.best = t; T.prim = first + k; T.aux = 0;
                             T.bu = u; T.bv = v;
@@ -319,13 +320,14 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
                     // Software-pipelined leaf: the next triangle's record loads while this one
                     // is tested (C3 -0.8%, C5 -1.0% at reduced spp, variants_leafpipe_*.log).
                     TriRec cur = load_tri(B.tris[T.start]);
+                    const bool q = B.tri_q && dir_tq(d);
                     for (uint32_t i = T.start; i < end; ++i) {
                         PH_COUNT(kPhLeafWave, kPhLeafLane);
                         TriRec nxt = cur;
                         if (i + 1 < end) nxt = load_tri(B.tris[i + 1]);
                         double t, u = 0.0, v = 0.0;
                         C.tri();
-                        const bool h = tri_uvt_r(cur, o, d, u, v, t);
+                        const bool h = tri_uvt_r<true>(cur, o, d, u, v, t, q);
                         if (h && (!T.valid || t < T.best)) {  // update_best_intersection (bvh.rs:213-222)
                             T.valid = true; T.best = t; T.prim = i; T.aux = 0;
                             T.bu = u; T.bv = v;
@@ -442,6 +444,7 @@ RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stk& S, Cnt<S
     if (!aabb_hit<FAST>(load3(B.root_min), load3(B.root_max), o, d, rc, t0)) return false;
     bool valid = false;
     double best = INFINITY;
+    const bool tq = KIND == 3 && B.tri_q && dir_tq(d);  // the split-division triangle solve
     if (B.depth == 1) {  // the root is the only leaf (bvh.rs:77, <= 4 primitives): [0, n_prims) in order
         // uniform index: the records come through the scalar cache
         const uint32_t np = uni_u32(B.n_prims);
@@ -451,7 +454,7 @@ RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stk& S, Cnt<S
             double t, u = 0.0, v = 0.0;
             uint32_t aux = 0;
             bool h;
-            if (KIND == 3) { C.tri(); const DevTri tr = tris[i]; h = tri_uvt(tr, o, d, u, v, t); }
+            if (KIND == 3) { C.tri(); const DevTri tr = tris[i]; h = tri_uvt(tr, o, d, u, v, t, tq); }
             else { C.shape(); const DevShape sh = shapes[i]; h = shape_closest<KIND>(sh, o, d, rc, FAST, t, aux); }
             if (h && (!valid || t < best)) {  // update_best_intersection (bvh.rs:213-222)
                 valid = true; best = t; bu = u; bv = v; bprim = i; baux = aux;
@@ -486,7 +489,7 @@ RT_D bool bvh_closest(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, Stk& S, Cnt<S
                     double t, u = 0.0, v = 0.0;
                     uint32_t aux = 0;
                     bool h;
-                    if (KIND == 3) { C.tri(); h = tri_uvt(B.tris[i], o, d, u, v, t); }
+                    if (KIND == 3) { C.tri(); h = tri_uvt(B.tris[i], o, d, u, v, t, tq); }
                     else { C.shape(); h = shape_closest<KIND>(B.shapes[i], o, d, rc, FAST, t, aux); }
                     if (h && (!valid || t < best)) {  // update_best_intersection (bvh.rs:213-222)
                         valid = true; best = t; bu = u; bv = v; bprim = i; baux = aux;
@@ -821,7 +824,7 @@ RT_D void leaf_all(const DevBvh& B, uint32_t start, uint32_t cnt, V3 o, V3 d, co
             DevTri tr;
             if (kUni) tr = uni(B.tris)[i];
             else tr = B.tris[i];
-            if (tri_uvt(tr, o, d, u, v, t)) {
+            if (tri_uvt(tr, o, d, u, v, t, B.tri_q && dir_tq(d))) {
                 V3 ng = load3(B.tri_cold[i].ng);  // sign flip (triangle.rs:76) cancels in |d.n|
                 impact += B.tri_inv_area[i] * (t * t / fabs(dot(d, ng)));
                 C.lhit(); nhits++;
@@ -2076,7 +2079,8 @@ __global__ void fp64_probe_kernel(const double* a, const double* b, double* out,
     out[i] = op == 0 ? sqrt(a[i])
            : op == 1 ? a[i] / b[i]
            : op == 2 ? dev_quot(a[i], b[i], dev_rcp(b[i]))
-           : op == 3 ? dev_sqrt(a[i]) : dev_inv_len(a[i]);
+           : op == 3 ? dev_sqrt(a[i])
+           : op == 4 ? dev_inv_len(a[i]) : dev_quotf(a[i], b[i], dev_rcp(b[i]));
 }
 
 // ------------------------------------------------------------- launch ----

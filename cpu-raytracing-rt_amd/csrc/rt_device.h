@@ -269,6 +269,15 @@ RT_D double dev_quotz(double x, double y, double r) {
     return x == 0.0 ? x * r : q;
 }
 
+// dev_quot finished with the division's own last step, v_div_fixup: it passes a
+// finite normal quotient through and returns x / y's signed zero for x == +-0
+// (dev_quot's last FMA gives +0 for x == -0, y > 0).  x / y's bits over
+// dev_quot's range and for x == +-0 in 4 ops (dev_quotz's compare-and-select
+// takes 6); checked against the host (test_dev_quot_matches_host, op 5).
+RT_D double dev_quotf(double x, double y, double r) {
+    return __builtin_amdgcn_div_fixup(dev_quot(x, y, r), y, x);
+}
+
 // sqrt(x) as the device computes it (render.hip ISA): for x < 2^-767 the compiler
 // pre-scales by 2^256, and 0 / +inf pass through a class test; for x in
 // [2^-767, +inf) both steps are identities and the result is this core — rsq,
@@ -438,7 +447,7 @@ RT_D bool plane_t(V3 n, V3 o, V3 d, double& t, uint32_t& aux) {
 // the plane's normal sign is +1 (one 32-bit word, so each max/min update of the
 // three axes selects three registers instead of five)
 struct Bpi { double t; uint32_t face; };
-// FD: shape_fast holds (d has no zero component; every quotient exact by dev_quotz)
+// FD: shape_fast holds (d has no zero component; every quotient exact by dev_quotf)
 template <bool FD = false>
 RT_D int box_coef(V3 s, V3 o, V3 d, const Rcp3& rc, Bpi& en, Bpi& ex) {
     bool have = false;
@@ -448,8 +457,8 @@ RT_D int box_coef(V3 s, V3 o, V3 d, const Rcp3& rc, Bpi& en, Bpi& ex) {
         if (!FD && di == 0.0 && si < fabs(oi)) return 0;
         if (!FD && di == 0.0) continue;
         const double ri = comp(rc.r, i);
-        double t1 = FD ? dev_quotz(si - oi, di, ri) : (si - oi) / di;
-        double t2 = FD ? dev_quotz(-si - oi, di, ri) : (-si - oi) / di;
+        double t1 = FD ? dev_quotf(si - oi, di, ri) : (si - oi) / di;
+        double t2 = FD ? dev_quotf(-si - oi, di, ri) : (-si - oi) / di;
         double a, b;
         uint32_t f;
         if (t1 < t2) { a = t1; b = t2; f = (uint32_t)i | 4u; } else { a = t2; b = t1; f = (uint32_t)i; }
@@ -527,28 +536,51 @@ RT_D TriRec load_tri(const DevTri& tr) {  // one batch of 16-B loads
     const double2 w0 = tw[0], w1 = tw[1], w2 = tw[2], w3 = tw[3], w4 = tw[4];
     return TriRec{v3(w0.x, w0.y, w1.x), v3(w1.y, w2.x, w2.y), v3(w3.x, w3.y, w4.x)};
 }
-RT_D bool tri_uvt_r(const TriRec& r, V3 o, V3 d, double& u, double& v, double& t) {
+// A direction whose triangle quotients may take the split division against a
+// compact record (Q below): every component 0 or |d_i| in [2^-240, 2^60).
+RT_D bool tq_ok(double v) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    return (b << 1) == 0 || (((uint32_t)(b >> 52) & 0x7ffu) - 783u) < 300u;
+}
+RT_D bool dir_tq(V3 d) { return tq_ok(d.x) && tq_ok(d.y) && tq_ok(d.z); }
+// Q && q: the record's edges are 0 or in [2^-149, 2^129) (differences of f32
+// vertices, the compact layout; DevBvh::tri_q otherwise) and dir_tq(d) holds.  Every product of two edge or edge and
+// direction components is then 0 or in [2^-389, 2^258], each cross-product
+// component (a difference of two such products: 0 or a multiple of the smaller
+// one's ulp) 0 or in [2^-441, 2^259], and |det| in [1e-11, 2^322] once the
+// degenerate test passed: the nine quotients c / det are in dev_quot's range
+// (or have a zero dividend), so one dev_rcp(det) and dev_quotf give x / y's bits
+// at 4 ops each instead of the full division's 11.
+template <bool Q = false>
+RT_D bool tri_uvt_r(const TriRec& r, V3 o, V3 d, double& u, double& v, double& t, bool q = false) {
     V3 m0 = r.ba, m1 = r.ca, m2 = -d;
     double det = m0.x * (m1.y * m2.z - m2.y * m1.z) - m1.x * (m0.y * m2.z - m2.y * m0.z) +
                  m2.x * (m0.y * m1.z - m1.y * m0.z);
     if (fabs(det) < 1e-11) return false;
     const V3 c0 = cross(m1, m2), c1 = cross(m2, m0), c2 = cross(m0, m1);
     V3 x0, x1, x2;
-    x0 = c0 / det; x1 = c1 / det; x2 = c2 / det;
+    if (Q && q) {
+        const double rr = dev_rcp(det);
+        x0 = v3(dev_quotf(c0.x, det, rr), dev_quotf(c0.y, det, rr), dev_quotf(c0.z, det, rr));
+        x1 = v3(dev_quotf(c1.x, det, rr), dev_quotf(c1.y, det, rr), dev_quotf(c1.z, det, rr));
+        x2 = v3(dev_quotf(c2.x, det, rr), dev_quotf(c2.y, det, rr), dev_quotf(c2.z, det, rr));
+    } else {
+        x0 = c0 / det; x1 = c1 / det; x2 = c2 / det;
+    }
     V3 w = o - r.a;
     double uu = dot(x0, w), vv = dot(x1, w), tt = dot(x2, w);
     if (uu < 0.0 || vv < 0.0 || 1.0 < uu + vv || tt < 0.0) return false;
     u = uu; v = vv; t = tt;
     return true;
 }
-RT_D bool tri_uvt(const DevTri& tr, V3 o, V3 d, double& u, double& v, double& t) {
+RT_D bool tri_uvt(const DevTri& tr, V3 o, V3 d, double& u, double& v, double& t, bool q = false) {
     // The whole record in one batch of 16-B loads; the asm keeps `a` from being
     // loaded only after the determinant and its early exit, which exposed a second
     // memory round trip per test (C3 -1.3%, C5 -1.4% at reduced spp,
     // profiles/r02/variants/variants_tripre_*.log).
     const TriRec r = load_tri(tr);
     asm volatile("" ::"v"(r.a.x), "v"(r.a.y), "v"(r.a.z));
-    return tri_uvt_r(r, o, d, u, v, t);
+    return tri_uvt_r<true>(r, o, d, u, v, t, q);
 }
 
 // Intersection (intersections.rs:10-16)

@@ -120,7 +120,8 @@ struct DevBvh {
     uint32_t n_prims;
     uint32_t depth;            // levels (root = 1)
     uint32_t fast;             // every box coordinate is 0 or in [2^-397, 2^400] (coord_fast)
-    uint32_t _pad;
+    uint32_t tri_q;            // every triangle edge component is 0 or in [2^-149, 2^129)
+                               // (rt_device.h tri_uvt_r: the split-division solve)
     // primitives in BVH order: exactly one of these is non-null
     const DevShape* shapes;
     const DevTri* tris;

@@ -408,6 +408,12 @@ void build_tri_bvh(const std::vector<TriItem>& items, HostBvhArrays& out, bool c
     if (compact && !h.nodes.empty()) build_compact(h, items, out);
     out.n_prims = (uint32_t)items.size();
     out.tris.reserve(items.size());
+    // DevBvh::tri_q: the edges' range of the split-division triangle solve
+    auto edge_ok = [](double v) { const double a = std::fabs(v); return a == 0.0 || (a >= 0x1p-149 && a < 0x1p129); };
+    out.tri_q = true;
+    for (const TriItem& it : items)
+        for (double v : {it.t.ba.x, it.t.ba.y, it.t.ba.z, it.t.ca.x, it.t.ca.y, it.t.ca.z})
+            out.tri_q = out.tri_q && edge_ok(v);
     for (uint64_t i : h.order) {
         const Triangle& t = items[i].t;
         DevTri d;

@@ -386,9 +386,10 @@ int rt_api_version(void);
 int rt_device_count(void);
 /* Diagnostic: device f64 sqrt (op 0), a/b (op 1), or the kernels' forms
    (rt_device.h): the split division dev_quot(a, b, dev_rcp(b)) (op 2), dev_sqrt(a)
-   (op 3) and dev_inv_len(a) = 1/sqrt(a) (op 4), for n values, to check that the
+   (op 3), dev_inv_len(a) = 1/sqrt(a) (op 4) and dev_quotf(a, b, dev_rcp(b)) (op 5,
+   the split division with the signed-zero fixup), for n values, to check that the
    device rounds like the host (the bit-exact parity premise).
-   b is read for ops 1 and 2 only. */
+   b is read for ops 1, 2 and 5 only. */
 int rt_probe_fp64(int op, const double* a, const double* b, uint32_t n, double* out);
 
 #ifdef __cplusplus

@@ -138,6 +138,13 @@ def test_dev_quot_matches_host(rt):
         bad = np.flatnonzero(got.view(np.uint64) != (x / y).view(np.uint64))
         assert bad.size == 0, [(x[i], y[i], got[i], x[i] / y[i]) for i in bad[:5]]
         assert np.array_equal(rt.probe_fp64(1, x, y), x / y)
+        # dev_quotf: the same pairs plus signed-zero dividends (the triangle and box
+        # quotients' form, rt_device.h)
+        z = np.resize(np.array([0.0, -0.0]), 4096)
+        xz, yz = np.concatenate([x, z]), np.concatenate([y, y[:z.size]])
+        got = rt.probe_fp64(5, xz, yz)
+        bad = np.flatnonzero(got.view(np.uint64) != (xz / yz).view(np.uint64))
+        assert bad.size == 0, [(xz[i], yz[i], got[i], xz[i] / yz[i]) for i in bad[:5]]
 
 
 def test_dev_sqrt_matches_host(rt):
