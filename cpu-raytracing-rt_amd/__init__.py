@@ -465,7 +465,7 @@ class Scene:
         _check(lib().rt_read_stats(self._h, C.byref(st), 1 if reset else 0))
         return st.as_dict()
 
-    def read_raw_stats(self, n: int = 48) -> np.ndarray:
+    def read_raw_stats(self, n: int = 64) -> np.ndarray:
         """Raw device counter words (diagnostics; rt_read_raw_stats)."""
         out = np.zeros(n, np.uint64)
         _check(lib().rt_read_raw_stats(self._h, out.ctypes.data_as(C.c_void_p), n))

@@ -669,7 +669,7 @@ int rt_read_stats(rt_scene* s, rt_stats* out, int reset) {
 }
 
 int rt_read_raw_stats(rt_scene* s, uint64_t* out, uint32_t n) {
-    if (!s || !out || n > (uint32_t)kStatsWords) return set_error(RT_ERR_INVALID, "scene/out NULL or n > 48");
+    if (!s || !out || n > (uint32_t)kStatsWords) return set_error(RT_ERR_INVALID, "scene/out NULL or n > 64");
     DEVICE_GUARD(s);
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(out, s->d_stats, n * sizeof(uint64_t), hipMemcpyDeviceToHost));

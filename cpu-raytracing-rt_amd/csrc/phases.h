@@ -10,15 +10,18 @@ namespace rt {
 // first active lane into LDS, flushed to raw stats words 16..23 (kPhase*).
 // The last four words count BVH traversal-loop iterations (wave-level and
 // summed over lanes) and primitive tests (wave-level inner-loop trips and
-// lane-level tests): their ratios are the loop's SIMD utilisation.
+// lane-level tests): their ratios are the loop's SIMD utilisation.  Wave
+// cycles inside the resumable walk's steps (trav_step): kPhLeafCyc the steps
+// that test leaf primitives, kPhInnerCyc the inner-node visits, kPhPopCyc the
+// stack pops, kPhStepCyc whole steps (kPhTris minus it: the loop around them).
 // Regions timed with PH_ADDW also add cycles x (active lanes / 64) at k + kPhW:
 // the ratio of the two is the region's lane utilisation.
 enum { kPhAssign, kPhIntersect, kPhLightSample, kPhLightPdf, kPhSegment, kPhCommit, kPhTile,
        kPhTravWave, kPhTravLane, kPhLeafWave, kPhLeafLane, kPhRngWave, kPhRngLane, kPhW0,
        kPhPlanes = kPhW0 + 5, kPhBoxes, kPhElls, kPhTris, kPhMaterialise,
        kPhInnerWave, kPhInnerLane, kPhLiveLane, kPhRngFallWave, kPhRngFallLane,
-       kPhPushLane, kPhPushGlobal, kPhPopGlobal, kPhN };  // traversal-stack pushes, past the LDS part
-static_assert(16 + kPhN <= 48, "phase words fit the raw stats");
+       kPhPushLane, kPhPushGlobal, kPhPopGlobal, kPhLeafCyc, kPhInnerCyc, kPhPopCyc, kPhStepCyc, kPhN };  // traversal-stack pushes, past the LDS part
+static_assert(16 + kPhN <= 64, "phase words fit the raw stats");
 constexpr int kPhW = kPhW0 - kPhIntersect;  // weighted word of region k = k + kPhW (k in 1..5)
 #ifdef RT_PHASES
 __shared__ unsigned long long g_phase[kPhN];

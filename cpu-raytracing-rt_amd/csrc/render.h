@@ -34,7 +34,7 @@ struct KParams {
 // device work counters: paths, segments, aabb, tri, shape, shaded, light queries,
 // light hits, lane steps, wave steps (64 x longest lane) — rt_stats order
 constexpr int kNStats = 10;
-constexpr int kStatsWords = 48;   // device counter words (rt_read_raw_stats)
+constexpr int kStatsWords = 64;   // device counter words (rt_read_raw_stats)
 constexpr int kStatLqSkip = 10;  // raw word: last-bounce light queries the timed kernel skips
 // raw words 11..13: inner-node visits of closest-hit traversals whose child boxes
 // were hit by none / one / both of the two slab tests (stats instances only)

@@ -285,12 +285,14 @@ RT_D TriRec load_tri_c(const float* __restrict__ p) {
 template <int KIND, int SLAB, bool ST, bool CMP = false, class Stk>
 RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk& S, Cnt<ST>& C, Trav& T,
                     uint64_t lv, int leaf_batch = kLeafBatch) {
+    const unsigned long long ph_st = PH_T();
     const uint64_t at_leaf = __ballot(T.live && T.cnt != 0);
     const bool do_leaves = at_leaf == lv || __popcll(at_leaf) >= leaf_batch;
     PH_COUNT(kPhTravWave, kPhTravLane);
     if (T.live) PH_LANE(kPhLiveLane);
     bool next = false;  // this lane finished its current node and pops
     if (do_leaves) {
+        const unsigned long long ph_l = PH_T();
         if (T.live && T.cnt != 0) {
             if constexpr (KIND == 3) {
                 const uint32_t end = T.start + T.cnt;
@@ -349,9 +351,11 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
             }
             next = true;
         }
+        PH_ADD(kPhLeafCyc, ph_l);
     } else if (CMP && T.live && T.cnt == 0) {  // internal node, compact layout (64 B)
         // both children's f32 boxes and their two child words (56 of the 64 B: a leaf's
         // own range is read by trav_enter)
+        const unsigned long long ph_i = PH_T();
         const float4* nw = (const float4*)(B.cnodes + T.node);
         const float4 w0 = nw[0], w1 = nw[1], w2 = nw[2];
         const uint2 k = ((const uint2*)nw)[6];
@@ -373,6 +377,7 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
             } else go_left = true;
         } else if (!(ri < bt)) next = true;
         if (!next) trav_enter<true>(B, T, go_left ? k.x : k.y);
+        PH_ADD(kPhInnerCyc, ph_i);
     } else if (!CMP && T.live && T.cnt == 0) {  // internal node (count 0 <=> children)
         PH_COUNT(kPhInnerWave, kPhInnerLane);
         const DevNode& n = B.nodes[T.node];
@@ -402,6 +407,7 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
         }
     }
     if (next) {  // resume from the stack: far children still closer than best
+        const unsigned long long ph_p = PH_T();
         bool found = false;
         uint32_t w = 0;
         while (S.sp > 0) {
@@ -411,7 +417,9 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
         }
         if (!found) T.live = false;
         else trav_enter<CMP>(B, T, w);
+        PH_ADD(kPhPopCyc, ph_p);
     }
+    PH_ADD(kPhStepCyc, ph_st);
 }
 
 // BVH::intersection (bvh.rs:27-36) + Node::intersection (bvh.rs:151-186) run

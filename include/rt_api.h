@@ -245,7 +245,7 @@ int rt_render_tiles_async(rt_scene* scene, const rt_render_params* params,
                           uint32_t rank, uint32_t world,
                           double* d_tile_rgb, void* hip_stream);
 
-/* Diagnostics: the scene's raw device counter words (n <= 48), accumulated by
+/* Diagnostics: the scene's raw device counter words (n <= 64), accumulated by
    RT_FLAG_STATS renders: words 0..9 are rt_stats' counters; word 10 counts the
    last-bounce light queries the timed (no-stats) kernel skips because they cannot
    be NaN (the stats render still runs them); words 11..13

@@ -694,6 +694,94 @@ def test_rotated_box_edges(rt, orc):
     _compare(g, o, params)
 
 
+# Shapes rotated about one coordinate axis (rt_device.h rotate_ax, kRotAxis): every
+# axis, both signs, a half turn (s = 0), a tiny angle, plus an emitting rotated box
+# and ellipsoid (the light-pdf walk) and a two-axis rotation (generic form).
+AXIS_ROT_SCENE = """DIMENSIONS 24 20
+SAMPLES 3
+RAY_DEPTH 8
+BG_COLOR 0.1 0.1 0.1
+CAMERA_POSITION 0 0 -2
+NEW_PRIMITIVE
+PLANE 0 1 0
+POSITION 0 -1 0
+COLOR 0.7 0.7 0.7
+NEW_PRIMITIVE
+BOX 0.25 0.5 0.125
+POSITION 0.25 -0.5 0.5
+ROTATION 0 0.17364817766693033 0 0.984807753012208
+COLOR 0.8 0.8 0.8
+NEW_PRIMITIVE
+BOX 0.2 0.1 0.3
+POSITION -0.5 0.5 0.25
+ROTATION -0.3826834323650898 0 0 0.9238795325112867
+COLOR 0.6 0.7 0.8
+NEW_PRIMITIVE
+BOX 0.125 0.25 0.2
+POSITION 0.5 0.5 -0.25
+ROTATION 0 0 1 0
+COLOR 0.5 0.5 0.5
+NEW_PRIMITIVE
+BOX 0.3 0.05 0.3
+POSITION 0 0.9 0
+ROTATION 0 0 0.25881904510252074 0.9659258262890683
+EMISSION 5 5 5
+NEW_PRIMITIVE
+BOX 0.2 0.2 0.2
+POSITION -0.25 -0.5 -0.5
+ROTATION 0 1e-20 0 1
+COLOR 0.9 0.4 0.4
+NEW_PRIMITIVE
+ELLIPSOID 0.25 0.5 0.375
+POSITION -0.5 -0.25 0.5
+ROTATION 0 0 -0.7071067811865476 0.7071067811865476
+EMISSION 2 3 4
+COLOR 0.3 0.3 0.3
+NEW_PRIMITIVE
+ELLIPSOID 0.2 0.3 0.1
+POSITION 0.5 0 0
+ROTATION 0.5 0.5 0 0.7071067811865476
+COLOR 0.9 0.9 0.9
+METALLIC
+"""
+
+
+def test_axis_rotation_edges(rt, orc):
+    """Boxes and ellipsoids rotated about one axis take the 11-operation rotation
+    (rt_device.h rotate_ax) for lanes whose o - pos and d have every component in
+    [2^-400, 2^401); others take the general form.  Rays from the shapes' centres
+    and dyadic points (zero o - pos components), with zero, tiny (below and above
+    2^-400) and huge direction components: hits, light sums and pdfs must equal the
+    oracle's bit for bit."""
+    desc, params = rt.parse_scene(AXIS_ROT_SCENE)
+    g, o = rt.Scene(desc), orc.OracleScene(desc)
+    rng = np.random.default_rng(33)
+    n = 40000
+    orig = rng.uniform(-0.9, 0.9, (n, 3))
+    orig[:4000] = rng.integers(-8, 9, (4000, 3)) / 8.0
+    orig[4000:6000] = [[0.25, -0.5, 0.5], [-0.5, 0.5, 0.25], [0.5, 0.5, -0.25], [0.0, 0.9, 0.0]][0]
+    d = rng.standard_normal((n, 3))
+    d[6000:8000, 1] = 0.0
+    d[8000:10000] *= np.array([1.0, 1e-125, 1.0])  # below rot_ok: general form
+    d[10000:12000] *= np.array([1e-110, 1.0, 1.0])  # tiny but in range
+    d[12000:14000] *= 1e300                          # above range
+    d[14000:16000] = rng.integers(-2, 3, (2000, 3)) / 2.0
+    d[14000:16000][np.all(d[14000:16000] == 0, axis=1)] = [0.0, 0.0, 1.0]
+    rays = np.concatenate([orig, d], axis=1)
+    gh, oh = g.intersect(rays), o.intersect(rays)
+    assert np.array_equal(gh.view(np.uint8), oh.view(np.uint8))
+    assert (gh["prim"] >= 0).sum() > n // 2
+    gi, gc = g.intersect_lights(rays)
+    oi, oc = o.intersect_lights(rays)
+    assert np.array_equal(gc, oc) and gc.sum() > 1000
+    assert np.array_equal(gi.view(np.uint64), oi.view(np.uint64))
+    fin = np.isfinite(np.linalg.norm(d, axis=1))
+    dn = d[fin] / np.linalg.norm(d[fin], axis=1, keepdims=True)
+    pd = np.concatenate([orig[fin], dn], axis=1)
+    assert np.array_equal(g.light_pdf(pd).view(np.uint64), o.light_pdf(pd).view(np.uint64))
+    _compare(g, o, params)
+
+
 def test_fast_shape_edges(rt, orc):
     """Identity-rotation shapes and signed-axis planes take the exact unguarded
     division for ray_fast rays (rt_device.h shape_fast, plane_axis_t).  Dyadic

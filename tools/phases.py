@@ -22,7 +22,7 @@ NAMES = ["assign", "intersect", "light_sample", "light_pdf", "segment", "commit"
          "w_intersect", "w_light_sample", "w_light_pdf", "w_segment", "w_commit",
          "isect_planes", "isect_boxes", "isect_ellipsoids", "isect_triangles", "isect_materialise",
          "inner_wave_iters", "inner_lane_iters", "live_lane_iters", "rng_fallback_wave", "rng_fallback_lane",
-         "push_lane", "push_global", "pop_global"]
+         "push_lane", "push_global", "pop_global", "leaf_cycles", "inner_cycles", "pop_cycles", "step_cycles"]
 rt = load_package()
 wl = sys.argv[1]
 scene_file, W, H, spp, depth = bench.WORKLOADS[wl]
@@ -31,7 +31,7 @@ if len(sys.argv) > 2:
 desc, params = bench.load_workload(rt, scene_file, W, H, spp)
 scene = rt.Scene(desc)
 _, _, st = scene.generate_image(params, stats=True)
-raw = scene.read_raw_stats(48)
+raw = scene.read_raw_stats(64)
 ph = {n: int(raw[16 + i]) for i, n in enumerate(NAMES)}
 tile = max(ph["tile"], 1)
 shading = ph["segment"] - ph["intersect"] - ph["light_sample"] - ph["light_pdf"]
@@ -40,6 +40,8 @@ share["shading_rest"] = shading / tile
 share["loop_other"] = 1.0 - ph["assign"] / tile - ph["segment"] / tile - ph["commit"] / tile
 for k in ("isect_planes", "isect_boxes", "isect_ellipsoids", "isect_triangles", "isect_materialise"):
     share[k] = ph[k] / tile
+for k in ("leaf", "inner", "pop", "step"):  # inside the resumable walk's steps (part of the walks above)
+    share["trav_" + k] = ph[k + "_cycles"] / tile
 print(json.dumps({"workload": wl, "spp": spp, "segments": st["segments"],
                   "lane_util": st["lane_steps"] / max(1, st["wave_steps"]),
                   "traversal_loop_util": ph["trav_lane_iters"] / max(1, 64 * ph["trav_wave_iters"]),
