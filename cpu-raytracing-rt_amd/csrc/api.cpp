@@ -263,13 +263,18 @@ int ensure_spill(rt_scene* s, uint64_t lanes, bool no_lds = false) {
 
 // Register budget of the path kernel for this scene.  Large BVHs make the loop
 // latency-bound on dependent node loads, where a 4th wave per SIMD hides more
-// than its register spill costs (C3: -9%); small scenes are VALU-bound and run
-// best at 3 (C2: +2% at 4).  rt_tuning.waves forces one (tests, tuning).
+// than its register spill costs (C3: -9%).  Shape-only scenes run the fused
+// kernel's shape-only instance at kShapeWaves (round 4: the path's T and L in
+// LDS and no LDS stack fit it in 128 VGPRs); other small scenes
+// run the general fused instance at 3.  rt_tuning.waves forces one (tests, tuning).
+bool path_resume(const rt_scene* s);
+int path_kinds(const rt_scene* s);
 uint32_t path_waves(const rt_scene* s) {
     if (s->tune.waves) return s->tune.waves;
     uint64_t nodes = 0;
     for (int k = 0; k < 6; ++k) nodes += s->info.bvh_nodes[k];
-    return nodes > kDeepSceneNodes ? 4u : 3u;
+    if (nodes > kDeepSceneNodes) return 4u;
+    return path_kinds(s) == 1 && !path_resume(s) ? kShapeWaves : 3u;
 }
 
 // Resumable triangle traversal (path_kernel RES) for scenes with a
@@ -353,7 +358,9 @@ int prepare_path(rt_scene* s, KParams& k, bool stats, bool hits, PathWork& W) {
     HIP_TRY(path_grid(stats, hits, W.waves, W.resume, W.kinds, (uint32_t)n_units, &W.grid, W.sorted));
     const uint64_t lanes = (uint64_t)W.grid * (W.sorted ? kSortLanes : 64u);
     int rc;
-    if ((rc = ensure_spill(s, lanes, W.sorted)) || (rc = ensure_part(s, k))) return rc;
+    // sort_kernel and the 4-wave shape-only fused kernel have no LDS stack
+    const bool no_lds = W.sorted || (W.waves == 4 && !W.resume && W.kinds == 1);
+    if ((rc = ensure_spill(s, lanes, no_lds)) || (rc = ensure_part(s, k))) return rc;
     if (!s->queue) HIP_TRY(hipMalloc(&s->queue, kQueueWords * sizeof(uint32_t)));
     const size_t ring_need = (size_t)W.grid * (W.sorted ? kSortRingRows : kRingRows) * 64 * 3;
     if (ring_need > s->ring_entries) {

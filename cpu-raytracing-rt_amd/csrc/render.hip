@@ -1177,6 +1177,18 @@ RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, P
         dir = degen ? h.ns : nrm(sw);
         const double cs = dot(dir, h.ns);
         if (cs <= 0.0) return false;
+        if (SLT && more && uni_u32(S.slt_mask)) {
+            // the light query's ray is the next segment's: defer the pdf to its box
+            // tests.  cosine_pdf = cs / pi here (cs > 0); above 2^-1000 the Mix pdf
+            // (cos + light) / 2 cannot be 0, so the path surely continues.
+            const double cp = cosine_pdf(h.ns, dir);
+            if (cp > 0x1p-1000) {
+                ps.pend = true; ps.pcos = cp; ps.pmat = mat;
+                ps.o = pos + dir * kEpsilon;
+                ps.d = dir;
+                return true;
+            }
+        }
         if (LT) {
             // The light query's ray (pos + dir * eps, dir; ray_sampler.rs:132-139) IS the
             // next segment's: set it first, so the old ray, the hit and the colour are dead
@@ -1200,18 +1212,6 @@ RT_D bool segment_shade(const DevScene& S, const KParams& P, const Scales& sc, P
             tl_mul_T(s_tl, diffuse_weight(load3(S.mats[mat].color), cp, pdf));
             if (last && (isnan(cs) || isnan(pdf))) tl_nan_L(s_tl);  // see below
             return true;
-        }
-        if (SLT && more && uni_u32(S.slt_mask)) {
-            // the light query's ray is the next segment's: defer the pdf to its box
-            // tests.  cosine_pdf = cs / pi here (cs > 0); above 2^-1000 the Mix pdf
-            // (cos + light) / 2 cannot be 0, so the path surely continues.
-            const double cp = cosine_pdf(h.ns, dir);
-            if (cp > 0x1p-1000) {
-                ps.pend = true; ps.pcos = cp; ps.pmat = mat;
-                ps.o = pos + dir * kEpsilon;
-                ps.d = dir;
-                return true;
-            }
         }
         double lp = 0.0;
         // On the path's last bounce only the pdf's NaN-ness is observable (below), and
@@ -1295,10 +1295,11 @@ RT_D bool segment_end(const DevScene& S, const KParams& P, const Scales& sc, Pat
                                                  s_tl);
 }
 
-// the fused form: one whole segment (scene_intersect to completion, then shade)
-template <bool ST, int KM = 3, class Stk>
+// the fused form: one whole segment (scene_intersect to completion, then shade);
+// LT as segment_shade's
+template <bool ST, int KM = 3, bool LT = false, class Stk>
 RT_D bool segment(const DevScene& S, const KParams& P, const Scales& sc, PathState& ps, Rng& rng, Stk& stk,
-                  Cnt<ST>& C, int32_t& hit_gid, bool more) {
+                  Cnt<ST>& C, int32_t& hit_gid, bool more, double* s_tl = nullptr) {
     Hit h; uint32_t mat; int32_t gid;
     C.segment();
     const unsigned long long ph0 = PH_T();
@@ -1308,11 +1309,14 @@ RT_D bool segment(const DevScene& S, const KParams& P, const Scales& sc, PathSta
         const uint32_t nl = S.n_lights;
         const double lp = nl == 1u ? impact : impact / (double)nl;
         const double pdf = (ps.pcos + lp) / 2.0;
-        ps.T = mul(ps.T, diffuse_weight(load3(S.mats[ps.pmat].color), ps.pcos, pdf));
+        const V3 w = diffuse_weight(load3(S.mats[ps.pmat].color), ps.pcos, pdf);
+        if (LT) tl_mul_T(s_tl, w);
+        else ps.T = mul(ps.T, w);
         ps.pend = false;
     }
     PH_ADDW(kPhIntersect, ph0);
-    return segment_shade<ST, Stk, true, KM>(S, P, sc, ps, rng, stk, C, hit, h, mat, gid, hit_gid, more, !more);
+    return segment_shade<ST, Stk, true, KM, LT>(S, P, sc, ps, rng, stk, C, hit, h, mat, gid, hit_gid, more, !more,
+                                                s_tl);
 }
 
 template <bool ST>
@@ -1433,10 +1437,13 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
     // radiance in LDS (kTL) — they are read only while a lane shades, so they do not
     // occupy registers (or scratch, where the 128-VGPR budget put them) across the
     // triangle traversal
-    constexpr int kS = (RES && WAVES == 4) ? kShortRes : kShort;
-    constexpr bool kTL = RES && WAVES == 4;
-    __shared__ uint32_t s_n[kS * kWave];
-    __shared__ double s_t[kS * kWave];
+    // (the 4-wave fused kernel of shape-only scenes: T/L in LDS too, and no LDS stack —
+    // the shapes' BVH walks push to the global spill stack, like sort_kernel's)
+    constexpr bool kW4S = !RES && WAVES == 4 && KM == kShapes;
+    constexpr int kS = (RES && WAVES == 4) ? kShortRes : (kW4S ? 0 : kShort);
+    constexpr bool kTL = (RES || kW4S) && WAVES == 4;
+    __shared__ uint32_t s_n[kS ? kS * kWave : 1];
+    __shared__ double s_t[kS ? kS * kWave : 1];
     __shared__ double s_tl[kTL ? 6 * kWave : 1];  // [T.x T.y T.z L.x L.y L.z][lane]
     __shared__ uint32_t s_cnt[kRing];  // finished paths per ring row
     // camera rays of the next kCamSlots paths, [component][slot] (fused kernel only)
@@ -1617,7 +1624,9 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
             if (b < depth) {
                 int32_t g;
                 const unsigned long long ph_s = PH_T();
-                cont = segment<ST, KM>(S, P, sc, ps, rng, stk, C, g, b + 1 < depth);
+                if constexpr (kTL) rng_rekey(rng, P.seed);
+                cont = segment<ST, KM, kTL>(S, P, sc, ps, rng, stk, C, g, b + 1 < depth, s_tl);
+                if constexpr (kTL) rng_park(rng);
                 PH_ADDW(kPhSegment, ph_s);
                 if (HIT) hit_ids[(pixel * P.spp + s) * depth + b] = g;
                 ++b;
@@ -2105,7 +2114,11 @@ template <bool ST, bool HIT>
 PathFn path_fn_r(uint32_t waves, bool resume, int kinds) {
 #ifdef RT_ONLY_C2  // experiment builds (tools/variants.py): only the C2 instances, 4x faster to compile
     (void)waves; (void)resume;
+#ifdef RT_C2_W4  // experiment: the shape-only fused kernel at 4 waves/SIMD
+    return kinds == kShapes ? path_kernel<ST, HIT, 4, false, kShapes> : path_kernel<ST, HIT, 3, false>;
+#else
     return kinds == kShapes ? path_kernel<ST, HIT, 3, false, kShapes> : path_kernel<ST, HIT, 3, false>;
+#endif
 #elif defined(RT_ONLY_C3)  // ... only the C3 instances
     (void)waves; (void)resume;
     if (kinds == kKindsCompact) return path_kernel<ST, HIT, 4, true, kTris, true>;
@@ -2116,7 +2129,7 @@ PathFn path_fn_r(uint32_t waves, bool resume, int kinds) {
         return kinds == kTris ? path_kernel<ST, HIT, 4, true, kTris> : path_kernel<ST, HIT, 4, true>;
     }
     kinds &= 3;  // the compact layout has only the triangle-only resumable instance (host: path_kinds)
-    if (waves == 4) return path_kernel<ST, HIT, 4, false>;
+    if (waves == 4) return kinds == kShapes ? path_kernel<ST, HIT, 4, false, kShapes> : path_kernel<ST, HIT, 4, false>;
     if (resume) return path_kernel<ST, HIT, 3, true>;
     return kinds == kShapes ? path_kernel<ST, HIT, 3, false, kShapes> : path_kernel<ST, HIT, 3, false>;
 #endif
