@@ -631,7 +631,11 @@ RT_D int box_test(const DevShape& s, V3 o, V3 d, const Rcp3& rc, bool rfast, Bpi
 #ifndef RT_NO_FASTSHAPE
     if (shape_fast(s, rfast, o, mo)) return box_coef<true>(load3(s.shape), mo, d, rc, en, ex);
 #endif
+#ifdef RT_EXP_ROTAX  // experiment: the one-axis rotation form
+    const bool same = model_ray<true>(s, o, d, mo, md);
+#else
     const bool same = model_ray(s, o, d, mo, md);
+#endif
     return box_model(s, mo, md, same, rc, en, ex);
 }
 // The Light::pdf callback terms of one light box crossing (leaf_all<1>:
@@ -1439,9 +1443,9 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
     // triangle traversal
     // (the 4-wave fused kernel of shape-only scenes: T/L in LDS too, and no LDS stack —
     // the shapes' BVH walks push to the global spill stack, like sort_kernel's)
-    constexpr bool kW4S = !RES && WAVES == 4 && KM == kShapes;
+    constexpr bool kW4S = !RES && WAVES >= 4 && KM == kShapes;
     constexpr int kS = (RES && WAVES == 4) ? kShortRes : (kW4S ? 0 : kShort);
-    constexpr bool kTL = (RES || kW4S) && WAVES == 4;
+    constexpr bool kTL = (RES && WAVES == 4) || kW4S;
     __shared__ uint32_t s_n[kS ? kS * kWave : 1];
     __shared__ double s_t[kS ? kS * kWave : 1];
     __shared__ double s_tl[kTL ? 6 * kWave : 1];  // [T.x T.y T.z L.x L.y L.z][lane]
@@ -2114,8 +2118,8 @@ template <bool ST, bool HIT>
 PathFn path_fn_r(uint32_t waves, bool resume, int kinds) {
 #ifdef RT_ONLY_C2  // experiment builds (tools/variants.py): only the C2 instances, 4x faster to compile
     (void)waves; (void)resume;
-#ifdef RT_C2_W4  // experiment: the shape-only fused kernel at 4 waves/SIMD
-    return kinds == kShapes ? path_kernel<ST, HIT, 4, false, kShapes> : path_kernel<ST, HIT, 3, false>;
+#ifdef RT_C2_W  // experiment: the shape-only fused kernel at RT_C2_W waves/SIMD
+    return kinds == kShapes ? path_kernel<ST, HIT, RT_C2_W, false, kShapes> : path_kernel<ST, HIT, 3, false>;
 #else
     return kinds == kShapes ? path_kernel<ST, HIT, 3, false, kShapes> : path_kernel<ST, HIT, 3, false>;
 #endif
