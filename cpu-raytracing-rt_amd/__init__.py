@@ -379,7 +379,7 @@ class Scene:
         return out
 
     def set_tuning(self, **kw):
-        """Force the kernel form of this scene's renders (rt_scene_set_tuning): waves (3|4),
+        """Force the kernel form of this scene's renders (rt_scene_set_tuning): waves (3|4|5; 5 = shape-only fused only),
         resume (0|1), kinds (3 = all-kinds instance), suspend_lanes, leaf_lanes (1..64),
         chunk_spp, compact (0 = f64 triangle-BVH layout, 1 = compact when the scene has it),
         sorted (1 = regrouped shading for shape-only fused scenes, 0 = the one-wave kernel).

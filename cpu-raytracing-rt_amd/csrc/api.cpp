@@ -265,16 +265,19 @@ int ensure_spill(rt_scene* s, uint64_t lanes, bool no_lds = false) {
 // latency-bound on dependent node loads, where a 4th wave per SIMD hides more
 // than its register spill costs (C3: -9%).  Shape-only scenes run the fused
 // kernel's shape-only instance at kShapeWaves (round 4: the path's T and L in
-// LDS and no LDS stack fit it in 128 VGPRs); other small scenes
-// run the general fused instance at 3.  rt_tuning.waves forces one (tests, tuning).
+// LDS and no LDS stack take it to 128 VGPRs without spill, and a 5th wave hides
+// more than its 42 VGPRs of spill cost); other small scenes run the
+// general fused instance at 3.  rt_tuning.waves forces one (tests, tuning); 5
+// exists for the shape-only fused form only (other forms take 4).
 bool path_resume(const rt_scene* s);
 int path_kinds(const rt_scene* s);
 uint32_t path_waves(const rt_scene* s) {
-    if (s->tune.waves) return s->tune.waves;
+    const bool shape_fused = path_kinds(s) == 1 && !path_resume(s);
+    if (s->tune.waves) return s->tune.waves == 5 && !shape_fused ? 4u : s->tune.waves;
     uint64_t nodes = 0;
     for (int k = 0; k < 6; ++k) nodes += s->info.bvh_nodes[k];
-    if (nodes > kDeepSceneNodes) return 4u;
-    return path_kinds(s) == 1 && !path_resume(s) ? kShapeWaves : 3u;
+    if (shape_fused) return kShapeWaves;
+    return nodes > kDeepSceneNodes ? 4u : 3u;
 }
 
 // Resumable triangle traversal (path_kernel RES) for scenes with a
@@ -358,8 +361,8 @@ int prepare_path(rt_scene* s, KParams& k, bool stats, bool hits, PathWork& W) {
     HIP_TRY(path_grid(stats, hits, W.waves, W.resume, W.kinds, (uint32_t)n_units, &W.grid, W.sorted));
     const uint64_t lanes = (uint64_t)W.grid * (W.sorted ? kSortLanes : 64u);
     int rc;
-    // sort_kernel and the 4-wave shape-only fused kernel have no LDS stack
-    const bool no_lds = W.sorted || (W.waves == 4 && !W.resume && W.kinds == 1);
+    // sort_kernel and the 4/5-wave shape-only fused kernel have no LDS stack
+    const bool no_lds = W.sorted || (W.waves >= 4 && !W.resume && W.kinds == 1);
     if ((rc = ensure_spill(s, lanes, no_lds)) || (rc = ensure_part(s, k))) return rc;
     if (!s->queue) HIP_TRY(hipMalloc(&s->queue, kQueueWords * sizeof(uint32_t)));
     const size_t ring_need = (size_t)W.grid * (W.sorted ? kSortRingRows : kRingRows) * 64 * 3;
@@ -618,7 +621,7 @@ int rt_scene_sample_chunks(const rt_scene* s, const rt_render_params* p, uint32_
 int rt_scene_set_tuning(rt_scene* s, const rt_tuning* t) {
     if (!s) return set_error(RT_ERR_INVALID, "scene is NULL");
     if (!t) { s->tune = rt_tuning{0, -1, 0, 0, 0, 0, -1, -1}; return RT_OK; }
-    if (t->waves != 0 && t->waves != 3 && t->waves != 4) return set_error(RT_ERR_INVALID, "waves must be 0, 3 or 4");
+    if (t->waves != 0 && (t->waves < 3 || t->waves > 5)) return set_error(RT_ERR_INVALID, "waves must be 0, 3, 4 or 5");
     if (t->resume < -1 || t->resume > 1) return set_error(RT_ERR_INVALID, "resume must be -1, 0 or 1");
     if (t->kinds > 3) return set_error(RT_ERR_INVALID, "kinds must be 0..3");
     // 1 / 2 (what rt_scene_get_tuning reports for a one-kind scene): only the scene's own kinds

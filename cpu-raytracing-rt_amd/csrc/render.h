@@ -112,7 +112,7 @@ constexpr uint32_t kSuspendCached = 32, kSuspendStreamed = 40;
 constexpr uint32_t kLeafCached = 32, kLeafStreamed = 24;
 constexpr uint64_t kCacheBytes = 256ull << 20;  // MI355X Infinity Cache (MALL)
 constexpr uint64_t kDeepSceneNodes = 4096;  // BVH nodes above which the 4-wave kernel runs
-constexpr uint32_t kShapeWaves = 4;  // waves/SIMD of the shape-only fused kernel (api.cpp path_waves)
+constexpr uint32_t kShapeWaves = 5;  // waves/SIMD of the shape-only fused kernel (api.cpp path_waves)
 constexpr size_t kQueueWords = 16;  // wave-tile counter (word 0), padded to a 64-B line
 
 hipError_t path_grid(bool stats, bool hits, uint32_t waves, bool resume, int kinds, uint32_t n_units,

@@ -1441,11 +1441,11 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
     // radiance in LDS (kTL) — they are read only while a lane shades, so they do not
     // occupy registers (or scratch, where the 128-VGPR budget put them) across the
     // triangle traversal
-    // (the 4-wave fused kernel of shape-only scenes: T/L in LDS too, and no LDS stack —
-    // the shapes' BVH walks push to the global spill stack, like sort_kernel's)
+    // (the fused kernel of shape-only scenes at 4-5 waves: T/L in LDS too, and no LDS
+    // stack — the shapes' BVH walks push to the global spill stack, like sort_kernel's)
     constexpr bool kW4S = !RES && WAVES >= 4 && KM == kShapes;
-    constexpr int kS = (RES && WAVES == 4) ? kShortRes : (kW4S ? 0 : kShort);
-    constexpr bool kTL = (RES && WAVES == 4) || kW4S;
+    constexpr int kS = (RES && WAVES >= 4) ? kShortRes : (kW4S ? 0 : kShort);
+    constexpr bool kTL = (RES && WAVES >= 4) || kW4S;
     __shared__ uint32_t s_n[kS ? kS * kWave : 1];
     __shared__ double s_t[kS ? kS * kWave : 1];
     __shared__ double s_tl[kTL ? 6 * kWave : 1];  // [T.x T.y T.z L.x L.y L.z][lane]
@@ -1460,7 +1460,6 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
     const KParams& Pt = WAVES == 3 ? *Pg : Pv;  // per-wave-tile constants
     const uint32_t depth = Pt.ray_depth;
     const uint32_t n_units = Pt.n_slots * Pt.chunks * 4u;
-    const uint64_t below = (1ull << lane) - 1ull;
     Cnt<ST> C;
     C.zero();
 #ifdef RT_PHASES
@@ -1540,7 +1539,9 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
                 }
                 __syncthreads();
             }
-            const uint32_t k = (uint32_t)__popcll(idle & below);
+            // idle lanes below this one (v_mbcnt: no lane mask held across the loop)
+            const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
             if (!busy && next + k < limit) {
                 cur = next + k;
                 const uint32_t row = cur / kWave, col = cur % kWave;
@@ -2125,7 +2126,11 @@ PathFn path_fn_r(uint32_t waves, bool resume, int kinds) {
 #endif
 #elif defined(RT_ONLY_C3)  // ... only the C3 instances
     (void)waves; (void)resume;
+#ifdef RT_C3_W  // experiment: the compact triangle-only kernel at RT_C3_W waves/SIMD
+    if (kinds == kKindsCompact) return path_kernel<ST, HIT, RT_C3_W, true, kTris, true>;
+#else
     if (kinds == kKindsCompact) return path_kernel<ST, HIT, 4, true, kTris, true>;
+#endif
     return kinds == kTris ? path_kernel<ST, HIT, 4, true, kTris> : path_kernel<ST, HIT, 4, true>;
 #else
     if (waves == 4 && resume) {
@@ -2133,6 +2138,7 @@ PathFn path_fn_r(uint32_t waves, bool resume, int kinds) {
         return kinds == kTris ? path_kernel<ST, HIT, 4, true, kTris> : path_kernel<ST, HIT, 4, true>;
     }
     kinds &= 3;  // the compact layout has only the triangle-only resumable instance (host: path_kinds)
+    if (waves == 5) return path_kernel<ST, HIT, 5, false, kShapes>;  // shape-only only (api.cpp path_waves)
     if (waves == 4) return kinds == kShapes ? path_kernel<ST, HIT, 4, false, kShapes> : path_kernel<ST, HIT, 4, false>;
     if (resume) return path_kernel<ST, HIT, 3, true>;
     return kinds == kShapes ? path_kernel<ST, HIT, 3, false, kShapes> : path_kernel<ST, HIT, 3, false>;

@@ -200,7 +200,9 @@ int rt_scene_get_info(const rt_scene* scene, rt_scene_info* out);
    property of the scene handle, reported by rt_scene_get_tuning, so every rank
    and process rendering one frame runs the same kernel instance. */
 typedef struct rt_tuning {
-    uint32_t waves;          /* 0 auto (4 when the BVHs hold > 4096 nodes, else 3); 3 or 4 waves/SIMD  */
+    uint32_t waves;          /* 0 auto (shape-only scenes 5; else 4 when the BVHs hold > 4096 nodes,
+                                else 3); 3, 4 or 5 waves/SIMD (5: the shape-only fused kernel only,
+                                other forms run 4 and report it) */
     int32_t  resume;         /* -1 auto (1 for a triangle BVH of > 4096 nodes); 0 fused segment,
                                 1 resumable triangle traversal                                          */
     uint32_t kinds;          /* 0 auto (the scene's primitive kinds); 3 the all-kinds instance; 1 or 2

@@ -181,9 +181,11 @@ def test_sorted_wide_frame(cornell, segment_form):
     _compare(g, o, params.replace(width=96, height=64, spp=9, ray_depth=20, seed=5))
 
 
-@pytest.mark.parametrize("waves", [3, 4])
+@pytest.mark.parametrize("waves", [3, 4, 5])
 def test_both_register_budgets(cornell, waves):
-    """Both path-kernel instances (3 and 4 waves/SIMD) are bit-exact (host picks per scene)."""
+    """Every register budget of the shape-only scene's fused kernel (3 waves/SIMD: the
+    general instance; 4 and 5: the shape-only instance with T/L in LDS) is bit-exact
+    (the host picks per scene)."""
     desc, params, g, o = cornell
     _compare(g, o, params.replace(width=40, height=24, spp=3, seed=3), waves=waves)
     assert g.tuning()["waves"] == waves
