@@ -2138,7 +2138,7 @@ PathFn path_fn_r(uint32_t waves, bool resume, int kinds) {
         return kinds == kTris ? path_kernel<ST, HIT, 4, true, kTris> : path_kernel<ST, HIT, 4, true>;
     }
     kinds &= 3;  // the compact layout has only the triangle-only resumable instance (host: path_kinds)
-    if (waves == 5) return path_kernel<ST, HIT, 5, false, kShapes>;  // shape-only only (api.cpp path_waves)
+    if (waves == 5 && !resume && kinds == kShapes) return path_kernel<ST, HIT, 5, false, kShapes>;  // api.cpp path_waves
     if (waves == 4) return kinds == kShapes ? path_kernel<ST, HIT, 4, false, kShapes> : path_kernel<ST, HIT, 4, false>;
     if (resume) return path_kernel<ST, HIT, 3, true>;
     return kinds == kShapes ? path_kernel<ST, HIT, 3, false, kShapes> : path_kernel<ST, HIT, 3, false>;
@@ -2178,7 +2178,7 @@ __global__ void stage_params_kernel(KParams* dst, KParams P) { *dst = P; }
 hipError_t launch_path(const DevScene& S, const KParams& P, const PathWork& W, double* out, int32_t* hit_ids,
                        unsigned long long* stats, hipStream_t st) {
     if (P.chunks == 0 || (P.chunks > 1 && !W.part) || !W.queue || !W.ring || W.grid == 0) return hipErrorInvalidValue;
-    if (W.waves != 3 && W.waves != 4) return hipErrorInvalidValue;
+    if (W.waves < 3 || W.waves > 5 || (W.waves == 5 && (W.resume || W.kinds != kShapes))) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(W.queue, 0, kQueueWords * sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
     // the frame constants travel by pointer (see opaque): stage them in the scene's

@@ -188,7 +188,10 @@ def test_both_register_budgets(cornell, waves):
     (the host picks per scene)."""
     desc, params, g, o = cornell
     _compare(g, o, params.replace(width=40, height=24, spp=3, seed=3), waves=waves)
-    assert g.tuning()["waves"] == waves
+    # 5 exists for the shape-only fused form only: the resumable and the all-kinds
+    # forms run (and report) 4
+    t = g.tuning()
+    assert t["waves"] == (4 if waves == 5 and not (t["kinds"] == 1 and t["resume"] == 0) else waves)
 
 
 @pytest.mark.parametrize("chunk_spp", [37, 1])

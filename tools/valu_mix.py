@@ -29,9 +29,9 @@ RATES = os.path.join(os.path.dirname(HERE), "profiles", "r04", "valu_rates_full.
 F64 = ("v_fma_f64", "v_fmac_f64", "v_mul_f64", "v_add_f64")
 TRANS64 = ("v_rcp_f64", "v_rsq_f64", "v_sqrt_f64", "v_frexp", "v_fract_f64", "v_rndne_f64", "v_trunc_f64",
            "v_floor_f64", "v_ceil_f64", "v_ldexp_f64")
-# product instances (render.hip path_fn_r): C2 shape-only fused (4 waves), the compact triangle-only
+# product instances (render.hip path_fn_r): C2 shape-only fused (5 waves), the compact triangle-only
 # resumable kernel (C3/C4/C5), the f64 triangle-only resumable kernel
-INSTANCES = {"C2": "path_kernel<false, false, 4, false, 1, false>",
+INSTANCES = {"C2": "path_kernel<false, false, 5, false, 1, false>",
              "C3": "path_kernel<false, false, 4, true, 2, true>",
              "tri_f64": "path_kernel<false, false, 4, true, 2, false>"}
 
