@@ -631,11 +631,7 @@ RT_D int box_test(const DevShape& s, V3 o, V3 d, const Rcp3& rc, bool rfast, Bpi
 #ifndef RT_NO_FASTSHAPE
     if (shape_fast(s, rfast, o, mo)) return box_coef<true>(load3(s.shape), mo, d, rc, en, ex);
 #endif
-#ifdef RT_EXP_ROTAX  // experiment: the one-axis rotation form
-    const bool same = model_ray<true>(s, o, d, mo, md);
-#else
     const bool same = model_ray(s, o, d, mo, md);
-#endif
     return box_model(s, mo, md, same, rc, en, ex);
 }
 // The Light::pdf callback terms of one light box crossing (leaf_all<1>:

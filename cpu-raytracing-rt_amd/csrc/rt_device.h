@@ -409,54 +409,11 @@ RT_D V3 rotate_fast(const Quat& q, bool ident, V3 v) {
     return rotate(q, v);
 }
 
-// Quaternion::rotate_vector for a rotation about axis K (q.v = a e_K, the
-// other two components ±0; kRotAxis), exactly.  With (I, J, K) cyclic the
-// general form's products by the zero components are signed zeros, and for
-// v with every component nonzero and in [2^-400, 2^401) (rot_ok), |a| in
-// [2^-100, 1] and s = 0 or |s| in [2^-100, 1], each one meets a nonzero term
-// (no product underflows) or only decides the sign of a zero that a later
-// `+ v` absorbs:
-//   tmp_J = a v_I + v_J s,  tmp_I = v_I s − a v_J,  tmp_K = v_K s,
-//   out_J = 2 (a tmp_I) + v_J,  out_I = v_I − 2 (a tmp_J),  out_K = v_K
-// (doubling is exact, so fma(p, ±2, v) rounds once where the general form
-// rounds 2p exactly and then the sum).  11 operations instead of 30; checked
-// against the oracle for every axis, signed zeros and range edges
-// (test_axis_rotation_edges).
-RT_D bool rot_ok(double v) {  // |v| in [2^-400, 2^401)
-    const uint32_t hi = (uint32_t)((uint64_t)__double_as_longlong(v) >> 32);
-    return ((hi >> 20) & 0x7ffu) - 623u < 801u;
-}
-RT_D bool rot_ok3(V3 v) { return rot_ok(v.x) && rot_ok(v.y) && rot_ok(v.z); }
-template <int K>
-RT_D V3 rotate_ax(double s, double a, V3 v) {
-    constexpr int I = (K + 1) % 3, J = (K + 2) % 3;
-    const double vi = comp(v, I), vj = comp(v, J);
-    const double tj = a * vi + vj * s;
-    const double ti = vi * s - a * vj;
-    const double oi = fma(a * tj, -2.0, vi), oj = fma(a * ti, 2.0, vj);
-    return K == 0 ? v3(v.x, oi, oj) : (K == 1 ? v3(oj, v.y, oi) : v3(oi, oj, v.z));
-}
-RT_D V3 rotate_axis(const DevShape& s, const Quat& r, V3 v) {  // s.axis is uniform: one scalar branch
-    const uint32_t k = s.axis & 3u;
-    return k == 0 ? rotate_ax<0>(r.s, r.v.x, v) : (k == 1 ? rotate_ax<1>(r.s, r.v.y, v) : rotate_ax<2>(r.s, r.v.z, v));
-}
-
 // model_space_ray (intersections.rs:93-99).  Returns true when md == d bit for
 // bit (identity rotation, d without zero components): the caller may then
 // reuse the world ray's direction reciprocals.
-// AX: lanes of a kRotAxis shape whose o - pos and d pass rot_ok take rotate_ax.
-template <bool AX = false>
 RT_D bool model_ray(const DevShape& s, V3 o, V3 d, V3& mo, V3& md) {
     Quat r = conjugate(load_quat(s.rot));
-    if (AX && (s.flags & kRotAxis)) {
-        // wave-uniform: a divergent form would keep both forms' results live
-        const V3 w = o - load3(s.pos);
-        if (__ballot(!(rot_ok3(w) && rot_ok3(d))) == 0) {
-            mo = rotate_axis(s, r, w);
-            md = rotate_axis(s, r, d);
-            return false;
-        }
-    }
     const bool ident = is_identity(r);
     mo = rotate_fast(r, ident, o - load3(s.pos));
     const bool same = ident && all_nonzero_finite(d);

@@ -86,14 +86,11 @@ struct alignas(16) DevShape {  // Primitive<T> hot part (scene.rs:20-27)
     // may then take dev_quot for this shape's quotients
     // (rt_device.h shape_fast).  kPlaneAxis: plane normal = sign * e_axis.
     uint32_t flags;
-    uint32_t axis;             // plane: 0..2, bit 2 = negative sign; kRotAxis: the rotation axis
+    uint32_t axis;             // plane: 0..2, bit 2 = negative sign
 };
 // kBoxSizes: a box whose half sizes are nonzero and in coord_fast range (any
 // rotation): box_model may then take dev_quot on the model-space ray.
-// kRotAxis: a rotation about one coordinate axis (rot.v = a e_axis, |a| in
-// [2^-100, 1], s = 0 or |s| in [2^-100, 1]): model_space_ray may take
-// rotate_ax (rt_device.h).
-constexpr uint32_t kShapeFast = 1u, kPlaneAxis = 2u, kBoxSizes = 4u, kRotAxis = 8u;
+constexpr uint32_t kShapeFast = 1u, kPlaneAxis = 2u, kBoxSizes = 4u;
 static_assert(sizeof(DevShape) == 112, "shape record");
 
 struct alignas(16) DevTri {    // Triangle hot part (triangle.rs:5-17)

@@ -275,18 +275,6 @@ static uint32_t shape_flags(const rt_shape& s, uint32_t& axis) {
     }
     if (s.type == RT_SHAPE_ELLIPSOID)  // radii in dev_quot's divisor range (rt_device.h dir_ok)
         for (int k = 0; k < 3; ++k) fast = fast && dir_ok_host(s.shape[k]);
-    if (s.type != RT_SHAPE_PLANE) {  // kRotAxis: one nonzero vector component of the rotation
-        auto mag_ok = [](double v) { const double a = std::fabs(v); return a >= 0x1p-100 && a <= 1.0; };
-        int zeros = 0, kr = -1;
-        for (int k = 0; k < 3; ++k) {
-            if (q[1 + k] == 0.0) zeros++;
-            else kr = k;
-        }
-        if (zeros == 2 && mag_ok(q[1 + kr]) && (q[0] == 0.0 || mag_ok(q[0]))) {
-            f |= kRotAxis;
-            axis = (uint32_t)kr;
-        }
-    }
     if (s.type == RT_SHAPE_PLANE) {
         int zeros = 0, k1 = -1;
         for (int k = 0; k < 3; ++k) {

@@ -699,9 +699,9 @@ def test_rotated_box_edges(rt, orc):
     _compare(g, o, params)
 
 
-# Shapes rotated about one coordinate axis (rt_device.h rotate_ax, kRotAxis): every
-# axis, both signs, a half turn (s = 0), a tiny angle, plus an emitting rotated box
-# and ellipsoid (the light-pdf walk) and a two-axis rotation (generic form).
+# Shapes rotated about one coordinate axis: every axis, both signs, a half turn
+# (s = 0), a tiny angle, plus an emitting rotated box and ellipsoid (the light-pdf
+# walk) and a two-axis rotation.
 AXIS_ROT_SCENE = """DIMENSIONS 24 20
 SAMPLES 3
 RAY_DEPTH 8
@@ -752,12 +752,11 @@ METALLIC
 
 
 def test_axis_rotation_edges(rt, orc):
-    """Boxes and ellipsoids rotated about one axis take the 11-operation rotation
-    (rt_device.h rotate_ax) for lanes whose o - pos and d have every component in
-    [2^-400, 2^401); others take the general form.  Rays from the shapes' centres
-    and dyadic points (zero o - pos components), with zero, tiny (below and above
-    2^-400) and huge direction components: hits, light sums and pdfs must equal the
-    oracle's bit for bit."""
+    """Rotated boxes and ellipsoids (model_space_ray through the quaternion rotation;
+    round 4 measured an 11-operation single-axis form against it).  Rays
+    from the shapes' centres and dyadic points (zero o - pos components), with zero,
+    tiny (below and above 2^-400) and huge direction components: hits, light sums and
+    pdfs must equal the oracle's bit for bit."""
     desc, params = rt.parse_scene(AXIS_ROT_SCENE)
     g, o = rt.Scene(desc), orc.OracleScene(desc)
     rng = np.random.default_rng(33)
@@ -767,7 +766,7 @@ def test_axis_rotation_edges(rt, orc):
     orig[4000:6000] = [[0.25, -0.5, 0.5], [-0.5, 0.5, 0.25], [0.5, 0.5, -0.25], [0.0, 0.9, 0.0]][0]
     d = rng.standard_normal((n, 3))
     d[6000:8000, 1] = 0.0
-    d[8000:10000] *= np.array([1.0, 1e-125, 1.0])  # below rot_ok: general form
+    d[8000:10000] *= np.array([1.0, 1e-125, 1.0])  # tiny components
     d[10000:12000] *= np.array([1e-110, 1.0, 1.0])  # tiny but in range
     d[12000:14000] *= 1e300                          # above range
     d[14000:16000] = rng.integers(-2, 3, (2000, 3)) / 2.0
