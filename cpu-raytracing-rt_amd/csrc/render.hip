@@ -301,7 +301,10 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
                     // next record widened (18 VGPRs) through the test, which the 4-wave
                     // kernel pays in spills (a traversal-only kernel needs 105 VGPRs with it,
                     // 84 without): C3 -0.9%, C5 -1.9% at reduced spp
-                    // (profiles/r03/variants/variants_leafpipe_C*.log).
+                    // (profiles/r03/variants/variants_leafpipe_C*.log); round 4, with the
+                    // spill gone, prefetching only the next record's raw f32 words (9
+                    // VGPRs) still loses: 3 -> 18 spilled VGPRs, C3 +1.5%, C5 +1.0%
+                    // (profiles/r04/variants_leafpf_C*.log).
                     // the leaf's block (rt_layout.h kLeafBlock): T.start is its index, the
                     // first word its first primitive, then the records in order
                     const float* blk = B.ctris + (size_t)T.start * kLeafBlock;
