@@ -61,7 +61,7 @@ for s in $STEPS; do
       run l2_$w 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum \
         --output-format csv -d "$OUT/l2_$w" -o run \
         -- $B --workload $w --steps 1 --warmup 0 --no-cpu-baseline --no-pmc || exit 1 ;;
-    phase2|phase3)  # per-region wave cycles from the -DRT_PHASES build (cpu-raytracing-rt_amd/ph_build)
+    phase2|phase3|phase5)  # per-region wave cycles from the -DRT_PHASES build (cpu-raytracing-rt_amd/ph_build)
       w=C${s#phase}
       RT_AMD_LIB=$PWD/cpu-raytracing-rt_amd/ph_build/librt_amd.so run phase_$w 600 \
         python3 tools/phases.py $w ${PHASE_SPP:-64} || exit 1 ;;
