@@ -90,7 +90,7 @@ def price(op, rates):
            ("v_ashr", "v_lshlrev_b32"), ("v_lshl", "v_lshlrev_b32"), ("v_mul", "v_mul_lo_u32"),
            ("v_mad_u32", "v_mul_lo_u32"), ("v_addc", "v_add_co_u32"), ("v_sub_co", "v_add_co_u32"),
            ("v_subb", "v_add_co_u32"), ("v_bfi", "v_bfe_u32"), ("v_alignbit", "v_bfe_u32"), ("v_bitop3", "v_bfe_u32"),
-           ("v_add3", "v_bfe_u32"), ("v_or3", "v_bfe_u32"), ("v_xad", "v_bfe_u32"), ("v_and_or", "v_bfe_u32"),
+           ("v_add3", "v_bfe_u32"), ("v_bitop3_b32", "v_bitop3_b32"), ("v_xor_b32", "v_xor_b32"), ("v_or3", "v_bfe_u32"), ("v_xad", "v_bfe_u32"), ("v_and_or", "v_bfe_u32"),
            ("v_add_lshl", "v_bfe_u32"), ("v_bcnt", "v_bfe_u32"), ("v_mbcnt", "v_bfe_u32"),
            ("v_sub_f32", "v_add_f32"), ("v_subrev_f32", "v_add_f32"), ("v_fmac_f32", "v_fma_f32"),
            ("v_rcp", "v_rcp_f64"), ("v_rsq", "v_rcp_f64"), ("v_sqrt", "v_rcp_f64"), ("v_trunc", "v_add_f32"),

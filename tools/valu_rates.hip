@@ -24,7 +24,7 @@ enum Op { FMA64, ADD64, MUL64, MAX64, RCP64, CMP64, FMA32, ADD32F, ADDU32, CNDMA
           LAT_FMA64, LAT_FMA32, LAT_RCP64,
           // round 4: the classes outside the f64 / int64 PMC counters ("other" in bench.py)
           MOV32, DPP, RFL, CVT64F32, CVT32F64, AND32, LSHL32, MULLO32, CMPU32, CMPCLS64, BFE32, ADDCO32,
-          DIVSCALE64, DIVFMAS64, DIVFIXUP64, CNDMASK_VCC, NOPS };
+          DIVSCALE64, DIVFMAS64, DIVFIXUP64, CNDMASK_VCC, XOR32, BITOP3, NOPS };
 static const char* kName[NOPS] = {"v_fma_f64", "v_add_f64", "v_mul_f64", "v_max_f64", "v_rcp_f64",
                                   "v_cmp_lt_f64", "v_fma_f32", "v_add_f32", "v_add_u32", "v_cndmask_b32",
                                   "v_mad_u64_u32", "f64 x/y (compiled)", "f64 sqrt (compiled)",
@@ -32,7 +32,8 @@ static const char* kName[NOPS] = {"v_fma_f64", "v_add_f64", "v_mul_f64", "v_max_
                                   "v_mov_b32", "v_mov_b32_dpp", "v_readfirstlane_b32", "v_cvt_f64_f32",
                                   "v_cvt_f32_f64", "v_and_b32", "v_lshlrev_b32", "v_mul_lo_u32", "v_cmp_gt_u32",
                                   "v_cmp_class_f64", "v_bfe_u32", "v_add_co_u32", "v_div_scale_f64",
-                                  "v_div_fmas_f64", "v_div_fixup_f64", "v_cndmask_b32 (vcc)"};
+                                  "v_div_fmas_f64", "v_div_fixup_f64", "v_cndmask_b32 (vcc)", "v_xor_b32",
+                                  "v_bitop3_b32"};
 
 #define R8(S) S S S S S S S S
 
@@ -126,6 +127,8 @@ __global__ __launch_bounds__(256) void rate_kernel(double* out, unsigned long lo
             asm volatile(R8("v_cmp_class_f64 vcc, %0, %1\n") : : "v"(a0), "v"(u1) : "vcc");
         }
         if constexpr (OP == BFE32) { U8("v_bfe_u32 %0, %0, 3, 7") }
+        if constexpr (OP == XOR32) { U8("v_xor_b32 %0, %0, %1") }
+        if constexpr (OP == BITOP3) { U8("v_bitop3_b32 %0, %0, %1, %1 bitop3:0x96") }
         if constexpr (OP == ADDCO32) {
             asm volatile(R8("v_add_co_u32 %0, vcc, %0, %1\n") : "+v"(u0) : "v"(u1) : "vcc");
         }
@@ -204,7 +207,8 @@ int main(int argc, char** argv) {
         run<MADU64>(8, cus); run<MOV32>(8, cus); run<DPP>(8, cus); run<RFL>(8, cus); run<CVT64F32>(8, cus);
         run<CVT32F64>(8, cus); run<AND32>(8, cus); run<LSHL32>(8, cus); run<MULLO32>(8, cus); run<CMPU32>(8, cus);
         run<CMPCLS64>(8, cus); run<BFE32>(8, cus); run<ADDCO32>(8, cus); run<DIVSCALE64>(8, cus);
-        run<DIVFMAS64>(8, cus); run<DIVFIXUP64>(8, cus); run<CNDMASK_VCC>(8, cus);
+        run<DIVFMAS64>(8, cus); run<DIVFIXUP64>(8, cus); run<CNDMASK_VCC>(8, cus); run<XOR32>(8, cus);
+        run<BITOP3>(8, cus);
         for (int w : {4}) {
             run<FMA64>(w, cus); run<CMP64>(w, cus); run<CNDMASK>(w, cus); run<MOV32>(w, cus); run<DPP>(w, cus);
             run<RFL>(w, cus); run<CVT64F32>(w, cus); run<AND32>(w, cus); run<CMPU32>(w, cus);
