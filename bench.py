@@ -14,6 +14,12 @@ per-frame segment count is counted on the device in an untimed pass.
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
+Without a torchrun environment, --gpus N > 1 starts the N ranks itself: torchrun
+as a child process (this process makes no HIP call first), whose rank 0 prints
+the line; its exit code is bench.py's.  Under torchrun, --gpus must equal
+WORLD_SIZE.  The line carries world_size_seen (dist.get_world_size()) and each
+rank's device (PCI id; distinct under nccl, or every rank exits non-zero).
+
 Rank 0 prints ONE JSON line.  Extras: "roofline" (the path kernel's f64 VALU
 issue roofline: PMC instruction mix of its launch over the chip's issue limit,
 timed by HIP events; plus its measured HBM rate and the SURVEY §8d algorithmic
@@ -133,6 +139,39 @@ def child_env(env):
     return out
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_plan(gpus, env, pmc_child=False):
+    """How this bench.py process runs for `--gpus N` (main.rs:94-111 is one frame over
+    every pixel; here N ranks, one per GPU, share it).  Returns one of
+      ("run", world)        render as rank RANK of WORLD_SIZE (1 when not under torchrun);
+      ("launch", n)         no torchrun environment and N > 1: start N ranks under
+                            torchrun as a CHILD process (never an exec) and relay its rc;
+      ("error", message)    --gpus disagrees with the torchrun world.
+    Decided from arguments and environment only: nothing here touches the GPU."""
+    if pmc_child:
+        return ("run", 1)
+    if gpus < 1:
+        return ("error", f"bench.py: --gpus {gpus}: need at least one GPU")
+    if "WORLD_SIZE" not in env:
+        return ("launch", gpus) if gpus > 1 else ("run", 1)
+    world = int(env["WORLD_SIZE"])
+    if world != gpus:
+        return ("error", f"bench.py: --gpus {gpus} but WORLD_SIZE={world}: the rank count must be the GPU "
+                         f"count asked for")
+    return ("run", world)
+
+
+def torchrun_cmd(n, argv, port):
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+
+
 def pmc_counters(args, world):
     """Counters of the timed path kernel's launch, from child rocprofv3 --pmc
     passes of this same workload (rank 0's tile share of a world-`world`
@@ -241,12 +280,18 @@ def valu_roofline(pmc, pmc_ns, kern_s, instance):
             "clock_GHz": clk_used / 1e9, "clock_measured_GHz": clk / 1e9,
             "active_lanes_per_instr": lanes, "lane_util": lanes / 64.0,
             "useful_lane_frac": frac * lanes / 64.0,
+            # the arithmetic roofline beside the issue one: f64 FMA/MUL/ADD lane-ops per second
+            # (instructions x the launch's mean active lanes) over the FP64 vector rate at
+            # the measured price, 64 lanes per 4.2 cycles on each of the 1024 SIMDs
+            "f64_arith_frac": f64 * lanes / kern_s / (64.0 / VALU_CYCLES["f64"] * SIMDS * clk_used),
+            "f64_instr_share": f64 / n,
             "hw_active_frac": 4.0 * pmc["SQ_ACTIVE_INST_VALU"] / avail,
             "peak_note": "peak = the same instruction mix issued back to back on all 1024 SIMDs at the measured "
                          "clock; frac = busy SIMD cycles (every class at its measured issue cost) / available; "
                          "frac_lower / frac_upper = the classes without their own rate at 2.3 / 4.2 cycles; "
                          "useful_lane_frac = frac x active lanes / 64 (divergence); hw_active_frac = "
-                         "SQ_ACTIVE_INST_VALU quad-cycles x 4 / available cycles",
+                         "SQ_ACTIVE_INST_VALU quad-cycles x 4 / available cycles; f64_arith_frac = f64 FMA/MUL/ADD "
+                         "lane-ops/s (x mean active lanes) / (64 / 4.2 x 1024 SIMDs x clock)",
         },
     }
 
@@ -267,23 +312,20 @@ def cpu_share():
                      "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
 
 
-def cpu_baseline(desc, params, target_s):
-    """Oracle (C restatement, kind "port") on a bounded window of rows at full spp,
-    on every host core this process may use (rayon uses all cores, main.rs:94)."""
-    sys.path.insert(0, os.path.join(HERE, "oracle"))
-    import oracle as orc
-    threads, host = cpu_share()
-    print(f"bench: cpu baseline: building the oracle scene on {threads} threads", file=sys.stderr, flush=True)
-    tb = time.perf_counter()
-    osc = orc.OracleScene(desc)  # the restated reference builder: outside the timed leg
-    build_s = time.perf_counter() - tb
-    # grow a centred band of rows in small slices until ~target_s of CPU work is
-    # done (the box's CPU share varies, so a one-shot calibration over- or
-    # under-shoots by several x); the rate is segments / time over all slices
-    mid = params.height // 2
-    r0 = r1 = mid
+def cpu_band(osc, params, threads, target_s, rows=None):
+    """One timed render of a centred band of rows at full spp.  rows=None grows the band
+    in small slices until ~target_s of CPU work is done (the box's CPU share varies, so a
+    one-shot calibration over- or under-shoots by several x); otherwise renders exactly
+    `rows`.  Returns (Msamples/s, (r0, r1), paths, segments, seconds)."""
     segs = paths = 0
     dt = 0.0
+    if rows is not None:
+        t = time.perf_counter()
+        _, _, st = osc.render(params, mode=0, threads=threads, rows=rows)
+        dt = time.perf_counter() - t
+        return st["segments"] / dt / 1e6, rows, st["paths"], st["segments"], dt
+    mid = params.height // 2
+    r0 = r1 = mid
     step = 2
     while dt < target_s and (r0 > 0 or r1 < params.height):
         lo, hi = max(0, r0 - step // 2), min(params.height, r1 + step - step // 2)
@@ -298,18 +340,51 @@ def cpu_baseline(desc, params, target_s):
         r0, r1 = lo, hi
         rate = (r1 - r0) / max(dt, 1e-3)  # rows per second so far
         step = int(max(2, min(2 * (r1 - r0), rate * (target_s - dt) / 2)))
-    return {
-        "value": segs / dt / 1e6,
-        "unit": "Msamples/s",
-        "cores": threads,
-        "host": host,
-        "oracle_build_s": build_s,
-        "kind": "port",
-        "sample": f"rows {r0}..{r1} of {params.width}x{params.height} at {params.spp} spp "
-                  f"({paths} paths, {segs} segments, {dt:.1f} s), recursive raytrace_impl, "
-                  f"OpenMP dynamic over pixels",
-        "seconds": dt,
-    }
+    return segs / dt / 1e6, (r0, r1), paths, segs, dt
+
+
+def cpu_baseline(desc, params, target_s, runs=3):
+    """Oracle (C restatement, kind "port") on a bounded window of rows at full spp, on
+    every host core this process may use (rayon uses all cores, main.rs:94).  Two builds
+    (SURVEY.md §8d): -O3 -march=native, compiled here on this host (`make -C oracle
+    native`), and the portable -O3 build that travels with the tree.  Each is timed
+    `runs` times on the same band (the first run sizes it to ~target_s / runs); the
+    reported rate is the median, with the spread.  value = the faster build's median
+    (the stricter baseline)."""
+    sys.path.insert(0, os.path.join(HERE, "oracle"))
+    import oracle as orc
+    threads, host = cpu_share()
+    out = {"unit": "Msamples/s", "cores": threads, "host": host, "kind": "port"}
+    rows = None
+    builds = {}
+    for variant in ("native", "portable"):
+        print(f"bench: cpu baseline ({variant}): building the oracle scene on {threads} threads",
+              file=sys.stderr, flush=True)
+        try:
+            tb = time.perf_counter()
+            osc = orc.OracleScene(desc, variant=variant)  # the restated reference builder: outside the timed leg
+            build_s = time.perf_counter() - tb
+        except Exception as e:  # noqa: BLE001  (no compiler for the native build: report it)
+            builds[variant] = {"error": f"{type(e).__name__}: {e}"}
+            continue
+        rates, secs = [], []
+        for _ in range(runs):
+            rate, rows, paths, segs, dt = cpu_band(osc, params, threads, target_s / runs, rows)
+            rates.append(rate)
+            secs.append(dt)
+        builds[variant] = {"median": float(np.median(rates)), "runs": rates, "seconds": secs,
+                           "spread": (max(rates) - min(rates)) / float(np.median(rates)),
+                           "oracle_build_s": build_s,
+                           "flags": "-O3 -march=native" if variant == "native" else "-O3 (portable)"}
+        del osc
+    ok = max((v for v in ("native", "portable") if "median" in builds.get(v, {})), key=lambda v: builds[v]["median"])
+    out["value"] = builds[ok]["median"]
+    out["value_build"] = ok
+    out["builds"] = builds
+    out["sample"] = (f"rows {rows[0]}..{rows[1]} of {params.width}x{params.height} at {params.spp} spp "
+                     f"({paths} paths, {segs} segments per run), recursive raytrace_impl, OpenMP dynamic over "
+                     f"pixels; median of {runs} runs per build")
+    return out
 
 
 def main():
@@ -319,7 +394,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default="C2", choices=sorted(WORKLOADS))
     ap.add_argument("--spp", type=int, default=None, help="override spp (not the headline config)")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=18.0, help="CPU work per oracle build (split over 3 runs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc child passes (roofline=null)")
     ap.add_argument("--as-rank0-of", type=int, default=0, help=argparse.SUPPRESS)  # PMC child: rank 0's share
@@ -330,7 +405,17 @@ def main():
                          "ranks share one GPU (a rehearsal of the N>1 path on a one-GPU box)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    plan, arg = rank_plan(args.gpus, os.environ, pmc_child=bool(args.as_rank0_of))
+    if plan == "error":
+        sys.exit(arg)
+    if plan == "launch":
+        # `python bench.py --gpus N`: N ranks under torchrun, started as a child (this
+        # process has made no HIP call), whose rank 0 prints the JSON line
+        import subprocess
+        cmd = torchrun_cmd(arg, sys.argv[1:], free_port())
+        print("bench: " + " ".join(cmd), file=sys.stderr, flush=True)
+        sys.exit(subprocess.run(cmd).returncode)
+    world = arg
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.as_rank0_of:  # a PMC child is a standalone process, whatever its environment says
@@ -441,12 +526,24 @@ def main():
                            float(np.mean([m[1].elapsed_time(m[2]) for m in ev])) if len(ev[0]) > 2 else 0.0,
                            float(np.mean([m[2].elapsed_time(m[3]) for m in ev])) if len(ev[0]) > 3 else 0.0],
                           dtype=torch.float64, device=dev)
+    # which device each rank rendered on (PCI domain:bus:device): under nccl every rank
+    # must own a distinct GPU, so the line proves RCCL saw N ranks on N devices
+    props = torch.cuda.get_device_properties(dev)
+    me = {"rank": rank, "local_rank": local, "hip_device": dev.index,
+          "pci": f"{props.pci_domain_id:04x}:{props.pci_bus_id:02x}:{props.pci_device_id:02x}",
+          "name": props.name}
     if world > 1:
         every = [torch.zeros_like(phases) for _ in range(world)]
         dist.all_gather(every, phases)
         per_rank = torch.stack(every).cpu().numpy()
+        devices = [None] * world
+        dist.all_gather_object(devices, me)
+        world_seen = dist.get_world_size()
     else:
         per_rank = phases.cpu().numpy()[None, :]
+        devices, world_seen = [me], 1
+    if args.dist_backend == "nccl" and len({d["pci"] for d in devices}) != world:  # every rank exits
+        sys.exit(f"bench.py: {world} nccl ranks but devices {[d['pci'] for d in devices]} are not distinct")
 
     if rank == 0 and part != world:  # PMC child: nothing to report
         return
@@ -488,6 +585,8 @@ def main():
             "value": value,
             "unit": "Msamples/s",
             "n_gpus": world,
+            "world_size_seen": world_seen,
+            "rank_devices": devices,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,

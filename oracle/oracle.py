@@ -16,19 +16,24 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
-_lib = None
+# "portable": -O3 (built once, travels with the tree); "native": -O3 -march=native,
+# built by `make native` on the machine that runs it (bench.py's cpu_baseline leg
+# builds it on the GPU box's host)
+LIB_PATHS = {"portable": LIB_PATH, "native": os.path.join(HERE, "build", "liboracle_native.so")}
+_libs = {}
 
 
-def build(quiet: bool = True):
-    subprocess.run(["make", "-C", HERE], check=True, capture_output=quiet)
+def build(quiet: bool = True, variant: str = "portable"):
+    subprocess.run(["make", "-C", HERE, "all" if variant == "portable" else "native"], check=True,
+                   capture_output=quiet)
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            build()
-        L = C.CDLL(LIB_PATH)
+def lib(variant: str = "portable"):
+    if variant not in _libs:
+        path = LIB_PATHS[variant]
+        if not os.path.exists(path) or variant == "native":  # native: always for this host's CPU
+            build(variant=variant)
+        L = C.CDLL(path)
         vp, dp, u32, u64, i32 = C.c_void_p, C.POINTER(C.c_double), C.c_uint32, C.c_uint64, C.c_int
         sig = {
             "oracle_scene_create": (vp, [vp]),
@@ -58,8 +63,8 @@ def lib():
         for name, (res, args) in sig.items():
             f = getattr(L, name)
             f.restype, f.argtypes = res, args
-        _lib = L
-    return _lib
+        _libs[variant] = L
+    return _libs[variant]
 
 
 def _d(a):
@@ -70,36 +75,37 @@ def _d(a):
 class OracleScene:
     """Scene::new restated on the CPU (oracle.c)."""
 
-    def __init__(self, desc):
+    def __init__(self, desc, variant: str = "portable"):
+        self._L = lib(variant)
         d, keep = desc.to_c()
-        self._h = lib().oracle_scene_create(C.byref(d))
+        self._h = self._L.oracle_scene_create(C.byref(d))
         del keep
         if not self._h:
             raise RuntimeError("oracle_scene_create failed")
 
     def __del__(self):
         if getattr(self, "_h", None):
-            lib().oracle_scene_destroy(self._h)
+            self._L.oracle_scene_destroy(self._h)
             self._h = None
 
     def bvh_info(self):
         n = np.zeros(6, np.uint64)
         dep = np.zeros(6, np.uint32)
-        lib().oracle_scene_bvh_info(self._h, n.ctypes.data, dep.ctypes.data)
+        self._L.oracle_scene_bvh_info(self._h, n.ctypes.data, dep.ctypes.data)
         return n, dep
 
     def bvh_dump(self, k: int):
-        n = int(lib().oracle_scene_bvh_dump(self._h, k, None, None))
+        n = int(self._L.oracle_scene_bvh_dump(self._h, k, None, None))
         links = np.zeros((n, 4), np.int64)
         bounds = np.zeros((n, 6), np.float64)
-        lib().oracle_scene_bvh_dump(self._h, k, links.ctypes.data, bounds.ctypes.data)
+        self._L.oracle_scene_bvh_dump(self._h, k, links.ctypes.data, bounds.ctypes.data)
         return links, bounds
 
     def bvh_prims(self, k: int):
         out = []
         i = 0
         while True:
-            g = lib().oracle_scene_bvh_prim(self._h, k, i)
+            g = self._L.oracle_scene_bvh_prim(self._h, k, i)
             if g < 0:
                 return out
             out.append(g)
@@ -120,7 +126,7 @@ class OracleScene:
         if hit_ids:
             hits = np.full((H * W, params.spp, params.ray_depth), -2, np.int32)
         st = _stats_struct()
-        rc = lib().oracle_render_chunked(self._h, C.byref(from_params), mode, threads, r0, r1, chunk_spp,
+        rc = self._L.oracle_render_chunked(self._h, C.byref(from_params), mode, threads, r0, r1, chunk_spp,
                                          img.ctypes.data, None if hits is None else hits.ctypes.data, C.byref(st))
         if rc != 0:
             raise RuntimeError(f"oracle_render failed: {rc}")
@@ -133,7 +139,7 @@ class OracleScene:
         mean = np.zeros((H, W, 3), np.float64)
         sq = np.zeros((H, W, 3), np.float64)
         st = _stats_struct()
-        rc = lib().oracle_render_moments(self._h, C.byref(params.to_c()), mode, threads, 0, H, mean.ctypes.data,
+        rc = self._L.oracle_render_moments(self._h, C.byref(params.to_c()), mode, threads, 0, H, mean.ctypes.data,
                                          sq.ctypes.data, C.byref(st))
         if rc != 0:
             raise RuntimeError(f"oracle_render_moments failed: {rc}")
@@ -143,20 +149,20 @@ class OracleScene:
         from importlib import import_module  # noqa: F401
         rays = np.ascontiguousarray(rays, np.float64).reshape(-1, 6)
         out = np.zeros(len(rays), HIT_DTYPE)
-        lib().oracle_intersect_rays(self._h, rays.ctypes.data, len(rays), out.ctypes.data)
+        self._L.oracle_intersect_rays(self._h, rays.ctypes.data, len(rays), out.ctypes.data)
         return out
 
     def intersect_lights(self, rays):
         rays = np.ascontiguousarray(rays, np.float64).reshape(-1, 6)
         imp = np.zeros(len(rays), np.float64)
         cnt = np.zeros(len(rays), np.uint32)
-        lib().oracle_intersect_lights_rays(self._h, rays.ctypes.data, len(rays), imp.ctypes.data, cnt.ctypes.data)
+        self._L.oracle_intersect_lights_rays(self._h, rays.ctypes.data, len(rays), imp.ctypes.data, cnt.ctypes.data)
         return imp, cnt
 
     def light_pdf(self, pos_dir):
         pos_dir = np.ascontiguousarray(pos_dir, np.float64).reshape(-1, 6)
         out = np.zeros(len(pos_dir), np.float64)
-        lib().oracle_light_pdf_rays(self._h, pos_dir.ctypes.data, len(pos_dir), out.ctypes.data)
+        self._L.oracle_light_pdf_rays(self._h, pos_dir.ctypes.data, len(pos_dir), out.ctypes.data)
         return out
 
 

@@ -49,3 +49,47 @@ def test_valu_roofline_prices_every_class():
     assert 3.5 < d["issue_cycles_per_instr"]["rest"] < 4.5 and 2.0 < d["issue_cycles_per_instr"]["int32"] < 4.3
     busy = 4.2 * 40 + 16.2 + 4.5 * 4 + sum(d["issue_cycles_per_instr"][k] * d[k] for k in ("int32", "cvt", "f32", "rest"))
     assert abs(d["busy_simd_cycles"] - busy) < 1e-9
+
+
+def test_gpus_flag_plans_the_ranks():
+    """`--gpus N` means N ranks: without torchrun, N > 1 launches them (torchrun as a child
+    process); under torchrun, --gpus must equal WORLD_SIZE; a PMC child is always one
+    standalone process."""
+    b = _bench()
+    assert b.rank_plan(1, {}) == ("run", 1)
+    assert b.rank_plan(8, {"PATH": "/usr/bin"}) == ("launch", 8)
+    assert b.rank_plan(8, {"WORLD_SIZE": "8", "RANK": "3"}) == ("run", 8)
+    kind, msg = b.rank_plan(8, {"WORLD_SIZE": "2"})
+    assert kind == "error" and "--gpus 8" in msg and "WORLD_SIZE=2" in msg
+    assert b.rank_plan(1, {"WORLD_SIZE": "4"})[0] == "error"  # the default --gpus 1 under a 4-rank torchrun
+    assert b.rank_plan(0, {})[0] == "error"
+    assert b.rank_plan(8, {"WORLD_SIZE": "8"}, pmc_child=True) == ("run", 1)
+    assert b.rank_plan(1, {}, pmc_child=True) == ("run", 1)
+
+
+def test_torchrun_child_command():
+    """The launch relays every argument to the ranks and pins the rendezvous to 127.0.0.1."""
+    b = _bench()
+    argv = ["--gpus", "4", "--steps", "5", "--dist-backend", "gloo"]
+    cmd = b.torchrun_cmd(4, argv, 29611)
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    i = cmd.index("--nproc-per-node")
+    assert cmd[i + 1] == "4"
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1" and cmd[cmd.index("--master-port") + 1] == "29611"
+    assert cmd[-len(argv):] == argv and cmd[-len(argv) - 1].endswith("bench.py")
+    p = b.free_port()
+    assert 0 < p < 65536
+
+
+def test_f64_arith_frac():
+    """The arithmetic roofline: f64 FMA/MUL/ADD lane-ops/s over 64 lanes per 4.2 cycles on 1024 SIMDs."""
+    b = _bench()
+    pmc = {"SQ_INSTS_VALU": 100.0, "SQ_INSTS_VALU_FMA_F64": 20.0, "SQ_INSTS_VALU_MUL_F64": 10.0,
+           "SQ_INSTS_VALU_ADD_F64": 10.0, "SQ_INSTS_VALU_TRANS_F64": 1.0, "SQ_INSTS_VALU_INT64": 4.0,
+           "SQ_INSTS_VALU_INT32": 10.0, "SQ_INSTS_VALU_CVT": 5.0, "SQ_INSTS_VALU_ADD_F32": 0.0,
+           "SQ_INSTS_VALU_MUL_F32": 0.0, "SQ_INSTS_VALU_FMA_F32": 0.0, "SQ_INSTS_VALU_TRANS_F32": 0.0,
+           "SQ_THREAD_CYCLES_VALU": 3000.0, "SQ_ACTIVE_INST_VALU": 100.0, "GRBM_GUI_ACTIVE": 8 * 2.0e9 * 1e-6}
+    d = b.valu_roofline(pmc, 1000, 1e-6, "C2")["valu_detail"]
+    want = 40 * 30 / 1e-6 / (64 / 4.2 * 1024 * 2.0e9)
+    assert abs(d["f64_arith_frac"] - want) < 1e-12 * want + 1e-18
+    assert d["f64_instr_share"] == 0.4
