@@ -662,15 +662,24 @@ static void node_closest(const BVH* b, uint64_t ni, V3 o, V3 d, Best* best, Coun
     double bt = best->valid ? best->h.t : INFINITY;
     double li = lh ? (lt < bt ? lt : bt) : bt;
     double ri = rh ? (rt < bt ? rt : bt) : bt;
+#ifdef ORACLE_NODE_HOOK /* experiment builds only (tools/f32slab_sim.c): observes, changes nothing */
+    ORACLE_NODE_HOOK(b, n, o, d, lh, lt, rh, rt, bt);
+#endif
     if (li < bt) {
         if (ri < bt) {
             if (li < ri) {
                 node_closest(b, (uint64_t)n->left, o, d, best, c);
                 double b2 = best->valid ? best->h.t : INFINITY;
+#ifdef ORACLE_POP_HOOK
+                ORACLE_POP_HOOK(b, n->right, o, d, ri, b2);
+#endif
                 if (ri < b2) node_closest(b, (uint64_t)n->right, o, d, best, c);
             } else {
                 node_closest(b, (uint64_t)n->right, o, d, best, c);
                 double b2 = best->valid ? best->h.t : INFINITY;
+#ifdef ORACLE_POP_HOOK
+                ORACLE_POP_HOOK(b, n->left, o, d, li, b2);
+#endif
                 if (li < b2) node_closest(b, (uint64_t)n->left, o, d, best, c);
             }
         } else {
