@@ -96,6 +96,7 @@ int upload_bvh(rt_scene* s, const HostBvhArrays& h, DevBvh& d) {
     d.depth = h.depth;
     d.fast = h.fast ? 1u : 0u;
     d.tri_q = h.tri_q ? 1u : 0u;
+    d.c32 = h.c32 ? 1u : 0u;
     if ((rc = upload(s, h.shapes, &d.shapes))) return rc;
     if ((rc = upload(s, h.tris, &d.tris))) return rc;
     if ((rc = upload(s, h.tri_cold, &d.tri_cold))) return rc;
@@ -244,7 +245,7 @@ int ensure_part(rt_scene* s, const KParams& k) {
 
 // Spill area for stack entries beyond the LDS short stack: depth bound of the
 // deepest BVH, one slot per launched lane (`no_lds`: a kernel without an LDS
-// stack, sort_kernel, spills every entry).
+// stack, the 4/5-wave shape-only fused kernel, spills every entry).
 int ensure_spill(rt_scene* s, uint64_t lanes, bool no_lds = false) {
     uint32_t depth = s->dev.max_depth;
     const uint32_t lds = no_lds ? 0u : (uint32_t)kMinShort;
@@ -263,12 +264,17 @@ int ensure_spill(rt_scene* s, uint64_t lanes, bool no_lds = false) {
 
 // Register budget of the path kernel for this scene.  Large BVHs make the loop
 // latency-bound on dependent node loads, where a 4th wave per SIMD hides more
-// than its register spill costs (C3: -9%).  Shape-only scenes run the fused
-// kernel's shape-only instance at kShapeWaves (round 4: the path's T and L in
-// LDS and no LDS stack take it to 128 VGPRs without spill, and a 5th wave hides
-// more than its 42 VGPRs of spill cost); other small scenes run the
-// general fused instance at 3.  rt_tuning.waves forces one (tests, tuning); 5
-// exists for the shape-only fused form only (other forms take 4).
+// than its register spill costs (C3: -9%).  Shape-only scenes with small shape
+// BVHs run the fused kernel's shape-only instance at kShapeWaves (round 4: the
+// path's T and L in LDS and no LDS stack take it to 128 VGPRs without spill, and
+// a 5th wave hides more than its 42 VGPRs of spill cost).  That
+// instance has no LDS stack: every push of a BVH walk goes to the global spill
+// stack, which a single-leaf BVH (the Cornell box's) never touches; so a
+// shape-only scene whose BVHs hold more than kShapeWavesNodes nodes runs the
+// 3-wave instance, whose 12-entry LDS stack takes the pushes (round 5, advisor
+// finding; measured in DESIGN.md §4).  Other small scenes run the general fused
+// instance at 3.  rt_tuning.waves forces one (tests, tuning); 5 exists for the
+// shape-only fused form only (other forms take 4).
 bool path_resume(const rt_scene* s);
 int path_kinds(const rt_scene* s);
 uint32_t path_waves(const rt_scene* s) {
@@ -276,7 +282,7 @@ uint32_t path_waves(const rt_scene* s) {
     if (s->tune.waves) return s->tune.waves == 5 && !shape_fused ? 4u : s->tune.waves;
     uint64_t nodes = 0;
     for (int k = 0; k < 6; ++k) nodes += s->info.bvh_nodes[k];
-    if (shape_fused) return kShapeWaves;
+    if (shape_fused) return nodes <= kShapeWavesNodes ? kShapeWaves : 3u;
     return nodes > kDeepSceneNodes ? 4u : 3u;
 }
 
@@ -312,15 +318,14 @@ bool path_compact(const rt_scene* s) {
     return s->tune.compact != 0 && s->dev.tris.cnodes && path_waves(s) == 4 && path_resume(s) && path_kinds(s) == 2;
 }
 
-// Regrouped shading (render.hip sort_kernel): the shape-only fused kernel with
-// the shading step dealt to the waves of a 4-wave workgroup by branch class.
-// rt_tuning.sorted forces it on (1) or off (0); it applies to shape-only scenes
-// on the fused segment form only (other scenes run path_kernel).
-bool sort_eligible(const rt_scene* s) { return path_kinds(s) == 1 && !path_resume(s); }
-bool path_sorted(const rt_scene* s) {
-    if (!sort_eligible(s)) return false;
-    return s->tune.sorted >= 0 ? s->tune.sorted == 1 : kSortAuto;
+// f32-decided child tests of the compact kernel (render.hip trav_step F32,
+// DESIGN.md §4): the same decisions as the f64 tests, made in f32 where a proven
+// bound settles them.  rt_tuning.slab32 forces it on (1) or off (0).
+bool path_slab32(const rt_scene* s) {
+    if (!path_compact(s) || !s->dev.tris.c32) return false;
+    return s->tune.slab32 >= 0 ? s->tune.slab32 == 1 : kSlab32Auto;
 }
+
 
 // Suspend threshold of the resumable traversal (render.h kSuspendCached /
 // kSuspendStreamed): by whether the triangle BVH and its hot records fit the
@@ -356,16 +361,15 @@ int prepare_path(rt_scene* s, KParams& k, bool stats, bool hits, PathWork& W) {
     std::memset(&W, 0, sizeof(W));
     W.waves = path_waves(s);
     W.resume = path_resume(s);
-    W.kinds = path_compact(s) ? kKindsCompact : path_kinds(s);
-    W.sorted = path_sorted(s);
-    HIP_TRY(path_grid(stats, hits, W.waves, W.resume, W.kinds, (uint32_t)n_units, &W.grid, W.sorted));
-    const uint64_t lanes = (uint64_t)W.grid * (W.sorted ? kSortLanes : 64u);
+    W.kinds = path_compact(s) ? (path_slab32(s) ? kKindsCompact32 : kKindsCompact) : path_kinds(s);
+    HIP_TRY(path_grid(stats, hits, W.waves, W.resume, W.kinds, (uint32_t)n_units, &W.grid));
+    const uint64_t lanes = (uint64_t)W.grid * 64u;
     int rc;
-    // sort_kernel and the 4/5-wave shape-only fused kernel have no LDS stack
-    const bool no_lds = W.sorted || (W.waves >= 4 && !W.resume && W.kinds == 1);
+    // the 4/5-wave shape-only fused kernel has no LDS stack
+    const bool no_lds = W.waves >= 4 && !W.resume && W.kinds == 1;
     if ((rc = ensure_spill(s, lanes, no_lds)) || (rc = ensure_part(s, k))) return rc;
     if (!s->queue) HIP_TRY(hipMalloc(&s->queue, kQueueWords * sizeof(uint32_t)));
-    const size_t ring_need = (size_t)W.grid * (W.sorted ? kSortRingRows : kRingRows) * 64 * 3;
+    const size_t ring_need = (size_t)W.grid * kRingRows * 64 * 3;
     if (ring_need > s->ring_entries) {
         if (int rc2 = ws_idle(s)) return rc2;
         if (s->ring) (void)hipFree(s->ring);
@@ -631,7 +635,9 @@ int rt_scene_set_tuning(rt_scene* s, const rt_tuning* t) {
     if (t->compact < -1 || t->compact > 1) return set_error(RT_ERR_INVALID, "compact must be -1, 0 or 1");
     if (t->compact == 1 && !s->dev.tris.cnodes)
         return set_error(RT_ERR_UNSUPPORTED, "compact = 1: the scene has no compact triangle layout");
-    if (t->sorted < -1 || t->sorted > 1) return set_error(RT_ERR_INVALID, "sorted must be -1, 0 or 1");
+    if (t->slab32 < -1 || t->slab32 > 1) return set_error(RT_ERR_INVALID, "slab32 must be -1, 0 or 1");
+    if (t->slab32 == 1 && !(s->dev.tris.cnodes && s->dev.tris.c32))
+        return set_error(RT_ERR_UNSUPPORTED, "slab32 = 1: the scene has no compact triangle layout within 2^60");
     s->tune = *t;
     return RT_OK;
 }
@@ -645,7 +651,7 @@ int rt_scene_get_tuning(const rt_scene* s, rt_tuning* out) {
     out->leaf_lanes = path_leaf_batch(s);
     out->chunk_spp = s->tune.chunk_spp;
     out->compact = path_compact(s) ? 1 : 0;
-    out->sorted = path_sorted(s) ? 1 : 0;
+    out->slab32 = path_slab32(s) ? 1 : 0;
     return RT_OK;
 }
 

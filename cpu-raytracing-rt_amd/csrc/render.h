@@ -69,6 +69,8 @@ inline void sample_chunks(uint32_t W, uint32_t H, uint32_t spp, uint32_t& chunks
 // compact layout (rt_layout.h DevNodeC): kTris | 4, only with the 4-wave
 // resumable instance (api.cpp path_kinds).
 constexpr int kKindsCompact = 6;
+constexpr int kKindsCompact32 = 14;  // kKindsCompact + f32-decided child tests (render.hip trav_step F32)
+constexpr bool kSlab32Auto = true;   // the host's pick for compact scenes (api.cpp path_slab32)
 
 // Device workspace of one path-kernel launch (owned by the scene).
 struct PathWork {
@@ -81,17 +83,9 @@ struct PathWork {
     uint32_t* queue;      // wave-tile counter, zeroed by launch_path
     double* ring;         // [grid][kRing=8][64][3] finished-path radiance
     double* part;         // [n_slots*chunks][256][3] chunk partial sums (chunks > 1)
-    uint32_t* spill_n;    // traversal-stack spill, stride grid*64 (grid*kSortLanes when sorted)
+    uint32_t* spill_n;    // traversal-stack spill, stride grid*64
     double* spill_t;
-    bool sorted;          // the regrouped-shading kernel (render.hip sort_kernel): shape-only fused scenes
 };
-// sort_kernel: workgroups of kSortLanes path slots, a commit window of kSortRingRows
-// rows per workgroup, no LDS stack (spill sized for the whole BVH depth)
-#ifndef RT_SORT_WAVES
-#define RT_SORT_WAVES 4
-#endif
-constexpr uint32_t kSortLanes = 64 * RT_SORT_WAVES, kSortRingRows = 16;
-constexpr bool kSortAuto = false;  // the host's pick for eligible scenes (api.cpp path_sorted)
 #ifndef RT_RING_ROWS
 #define RT_RING_ROWS 8
 #endif
@@ -113,10 +107,11 @@ constexpr uint32_t kLeafCached = 32, kLeafStreamed = 24;
 constexpr uint64_t kCacheBytes = 256ull << 20;  // MI355X Infinity Cache (MALL)
 constexpr uint64_t kDeepSceneNodes = 4096;  // BVH nodes above which the 4-wave kernel runs
 constexpr uint32_t kShapeWaves = 5;  // waves/SIMD of the shape-only fused kernel (api.cpp path_waves)
+constexpr uint64_t kShapeWavesNodes = 64;  // BVH nodes of a shape-only scene up to which it runs at kShapeWaves
 constexpr size_t kQueueWords = 16;  // wave-tile counter (word 0), padded to a 64-B line
 
 hipError_t path_grid(bool stats, bool hits, uint32_t waves, bool resume, int kinds, uint32_t n_units,
-                     uint32_t* grid, bool sorted = false);
+                     uint32_t* grid);
 hipError_t launch_path(const DevScene& S, const KParams& P, const PathWork& W, double* out, int32_t* hit_ids,
                        unsigned long long* stats, hipStream_t st);
 hipError_t launch_reduce_chunks(const double* part, double* out, const KParams& P, hipStream_t st);

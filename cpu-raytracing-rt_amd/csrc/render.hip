@@ -282,9 +282,22 @@ RT_D TriRec load_tri_c(const float* __restrict__ p) {
 // CMP: the triangle BVH's compact layout (DevBvh::cnodes / ctris, KIND 3 only):
 // the same boxes and vertices as exact f32 copies, widened to f64 before the
 // same arithmetic — every lane's visits, tests and results are the f64 form's.
-template <int KIND, int SLAB, bool ST, bool CMP = false, class Stk>
+// F32 (compact layout only): the inner node's child tests are decided in f32
+// (rt_device.h slab32, Ray32 *R) and the f64 tests run only for lanes whose
+// decision the f32 bound leaves open — the f64 test's decisions either way.
+#ifndef RT_SLAB32_PAIR
+#define RT_SLAB32_PAIR 1
+#endif
+constexpr bool kSlabPair = RT_SLAB32_PAIR != 0;
+// f32 bounds on either side of the f64 best: blo <= best <= bhi
+RT_D void best32(double best, float& blo, float& bhi) {
+    const float b = (float)best;
+    blo = b * (1.0f - 0x1p-22f);
+    bhi = b * (1.0f + 0x1p-22f);
+}
+template <int KIND, int SLAB, bool ST, bool CMP = false, bool F32 = false, class Stk>
 RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk& S, Cnt<ST>& C, Trav& T,
-                    uint64_t lv, int leaf_batch = kLeafBatch) {
+                    uint64_t lv, int leaf_batch = kLeafBatch, const Ray32* R = nullptr) {
     const unsigned long long ph_st = PH_T();
     const uint64_t at_leaf = __ballot(T.live && T.cnt != 0);
     const bool do_leaves = at_leaf == lv || __popcll(at_leaf) >= leaf_batch;
@@ -364,21 +377,59 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
         const uint2 k = ((const uint2*)nw)[6];
         asm volatile("" ::"v"(w1.z), "v"(w1.w), "v"(w2.x), "v"(w2.y), "v"(w2.z), "v"(w2.w));  // see node_boxes
         PH_COUNT(kPhInnerWave, kPhInnerLane);
-        double lt = 0.0, rt2 = 0.0;
         C.aabb(2);
-        const bool lh = slab_c<SLAB>(w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, o, d, rc, fast, lt);
-        const bool rh = slab_c<SLAB>(w1.z, w1.w, w2.x, w2.y, w2.z, w2.w, o, d, rc, fast, rt2);
-        C.kids(lh, rh);
-        const double bt = T.best;  // +inf when no hit yet
-        const double li = lh ? (lt < bt ? lt : bt) : bt;
-        const double ri = rh ? (rt2 < bt ? rt2 : bt) : bt;
-        bool go_left = false;
-        if (li < bt) {
-            if (ri < bt) {
-                if (li < ri) { S.push(k.y, ri); go_left = true; }
-                else S.push(k.x, li);
-            } else go_left = true;
-        } else if (!(ri < bt)) next = true;
+        bool go_left = false, push = false;
+        uint32_t pw = 0;
+        double pt = 0.0;
+        bool exact = true;
+        if constexpr (F32) {
+            exact = !(R->E >= 0.0f);  // a ray that does not qualify: every test in f64
+            if (!exact) {
+                float vl, ml, vr, mr, blo, bhi;
+                bool zl, zr;
+                const int cl = slab32<kSlabPair>(w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, *R, vl, ml, zl);
+                const int cr = slab32<kSlabPair>(w1.z, w1.w, w2.x, w2.y, w2.z, w2.w, *R, vr, mr, zr);
+                best32(T.best, blo, bhi);
+                // v's interval (exactly 0 when z)
+                const float lhi = zl ? 0.0f : vl + ml, llo = zl ? 0.0f : vl - ml;
+                const float rhi = zr ? 0.0f : vr + mr, rlo = zr ? 0.0f : vr - mr;
+                // visit <=> hit && v < best (bvh.rs:161-165), decided either way or open
+                const bool lvis = cl == 1 && lhi < blo, lskip = cl == 0 || (cl == 1 && llo >= bhi);
+                const bool rvis = cr == 1 && rhi < blo, rskip = cr == 0 || (cr == 1 && rlo >= bhi);
+                exact = !(lvis || lskip) || !(rvis || rskip);
+                if (!exact) {
+                    if (lvis && rvis) {  // near first: left <=> v_l < v_r (bvh.rs:167)
+                        if (lhi < rlo) {
+                            push = true; pw = k.y; go_left = true;
+                            pt = zr ? 0.0 : stk_f32(vr, T.node, 1u);
+                        } else if (llo >= rhi) {
+                            push = true; pw = k.x;
+                            pt = zl ? 0.0 : stk_f32(vl, T.node, 0u);
+                        } else exact = true;
+                    } else if (lvis) go_left = true;
+                    else if (!rvis) next = true;
+                }
+                if (!exact) C.kids(cl == 1, cr == 1);
+            }
+        }
+        if (exact) {  // the f64 tests (bvh.rs:158-185)
+            double lt = 0.0, rt2 = 0.0;
+            const bool lh = slab_c<SLAB>(w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, o, d, rc, fast, lt);
+            const bool rh = slab_c<SLAB>(w1.z, w1.w, w2.x, w2.y, w2.z, w2.w, o, d, rc, fast, rt2);
+            C.kids(lh, rh);
+            const double bt = T.best;  // +inf when no hit yet
+            const double li = lh ? (lt < bt ? lt : bt) : bt;
+            const double ri = rh ? (rt2 < bt ? rt2 : bt) : bt;
+            if (li < bt) {
+                if (ri < bt) {
+                    push = true;
+                    // v >= 0 (or -0): + 0.0 clears the sign bit the f32 entries use (F32)
+                    if (li < ri) { pw = k.y; pt = ri + 0.0; go_left = true; }
+                    else { pw = k.x; pt = li + 0.0; }
+                } else go_left = true;
+            } else if (!(ri < bt)) next = true;
+        }
+        if (push) S.push(pw, pt);
         if (!next) trav_enter<true>(B, T, go_left ? k.x : k.y);
         PH_ADD(kPhInnerCyc, ph_i);
     } else if (!CMP && T.live && T.cnt == 0) {  // internal node (count 0 <=> children)
@@ -416,6 +467,23 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
         while (S.sp > 0) {
             double tt;
             S.pop(w, tt);
+            if constexpr (F32) {
+                const int hw = __double2hiint(tt);
+                if (hw < 0) {  // an f32-decided entry (stk_f32): v' within eps v' + E
+                    const float v = __int_as_float(__double2loint(tt));
+                    const float m = fmaf(kEps32, v, R->E);
+                    float blo, bhi;
+                    best32(T.best, blo, bhi);
+                    if (v + m < blo) { found = true; break; }
+                    if (v - m >= bhi) continue;
+                    // open: the f64 test of that child, its box from the parent's line
+                    const float* bx = (const float*)(B.cnodes + (((uint32_t)hw >> 1) & 0x3FFFFFFFu)) + (hw & 1) * 6;
+                    double t = 0.0;
+                    (void)slab_c<SLAB>(bx[0], bx[1], bx[2], bx[3], bx[4], bx[5], o, d, rc, fast, t);
+                    if (t < T.best) { found = true; break; }
+                    continue;
+                }
+            }
             if (tt < T.best) { found = true; break; }
         }
         if (!found) T.live = false;
@@ -1082,19 +1150,21 @@ struct SegQuery {
     Cand best;
     Trav T;
     bool fast;  // unguarded slab division for the triangle BVH (DevBvh::fast && ray_fast)
+    Ray32 r32;  // the ray's f32 form for the f32-decided child tests (path_kernel F32)
 };
 
 // raytrace_impl's `intersect` call (raytrace.rs:13), first part: planes,
 // boxes and ellipsoids to completion, then the triangle traversal is set up.
 // KM == kTris (a triangle-only scene): no shapes to test, and the candidate is
 // the triangle traversal's alone (q.best is not carried across the loop)
-template <bool ST, int KM = 3, class Stk>
+template <bool ST, int KM = 3, bool F32 = false, class Stk>
 RT_D void segment_begin(const DevScene& S, const PathState& ps, Stk& stk, Cnt<ST>& C, SegQuery& q) {
     C.segment();
     q.rc = make_rcp3(ps.d);
     const bool rfast = ray_fast(ps.o, q.rc);
     if (KM != kTris) shapes_closest<ST, true>(S, ps.o, ps.d, q.rc, rfast, stk, C, q.best);
     q.fast = S.tris.fast && rfast;
+    if (F32) ray32_make(ps.o, ps.d, q.rc, q.fast && S.tris.c32, q.r32);
     trav_init<2, ST>(S.tris, ps.o, ps.d, q.rc, q.fast, stk, C, q.T);
 }
 
@@ -1428,7 +1498,7 @@ RT_D uint32_t unit_of_row(const uint32_t* uq, uint32_t uq_back, uint32_t row) {
 }
 
 
-template <bool ST, bool HIT, int WAVES, bool RES, int KM = 3, bool CMP = false>
+template <bool ST, bool HIT, int WAVES, bool RES, int KM = 3, bool CMP = false, bool F32 = false>
 __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams Pv,
                                                      const DevScene* __restrict__ Sg,
                                                      const KParams* __restrict__ Pg, double* __restrict__ out,
@@ -1441,7 +1511,7 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
     // occupy registers (or scratch, where the 128-VGPR budget put them) across the
     // triangle traversal
     // (the fused kernel of shape-only scenes at 4-5 waves: T/L in LDS too, and no LDS
-    // stack — the shapes' BVH walks push to the global spill stack, like sort_kernel's)
+    // stack — the shapes' BVH walks push to the global spill stack)
     constexpr bool kW4S = !RES && WAVES >= 4 && KM == kShapes;
     constexpr int kS = (RES && WAVES >= 4) ? kShortRes : (kW4S ? 0 : kShort);
     constexpr bool kTL = (RES && WAVES >= 4) || kW4S;
@@ -1585,7 +1655,7 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
             // lanes between segments (new paths, continued paths) start their query
             const unsigned long long ph_b = PH_T();
             if (busy && !inq && b < depth) {
-                segment_begin<ST, KM>(S, ps, stk, C, q);
+                segment_begin<ST, KM, F32>(S, ps, stk, C, q);
                 inq = true;
             }
             PH_ADDW(kPhIntersect, ph_b);
@@ -1602,7 +1672,8 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
                     const bool can_take = next < min(win, open_end * kWave) || (!drained && next < win);
                     if (__ballot((busy && !q.T.live) || (!busy && can_take))) break;
                 }
-                trav_step<3, 2, ST, CMP>(S.tris, ps.o, ps.d, q.rc, q.fast, stk, C, q.T, lv, (int)P.leaf_batch);
+                trav_step<3, 2, ST, CMP, F32>(S.tris, ps.o, ps.d, q.rc, q.fast, stk, C, q.T, lv, (int)P.leaf_batch,
+                                              &q.r32);
             }
             PH_ADD(kPhTris, ph_t);
             // lanes whose query finished shade and end (or continue) their segment
@@ -1679,288 +1750,6 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
 #ifdef RT_PHASES
     if (ST && lane < kPhN) atomicAdd(&stats[kPhaseWord0 + lane], g_phase[lane]);
 #endif
-}
-
-// sort_kernel — the shape-only fused segment (every custom-format scene: C1/C2)
-// with its shading step REGROUPED across a 4-wave workgroup (round 4, DESIGN.md §4
-// "regrouped shading").  In the one-wave kernel every wave runs the union of its
-// lanes' shading branches — dielectric, metallic, the Mix sampler's cosine and light
-// branches — at ~31 of 64 active lanes; shading one branch class per wave measured
-// +24.5% segments/s at the same lane work (variants_bound_C2.log).  Here a path
-// lives in an LDS slot of its workgroup, not in a lane:
-//   A  idle slots take the next (sample row, pixel) paths of the workgroup's stream;
-//   B  every lane intersects the path of its slot (scene_intersect, the previous
-//      diffuse bounce's light pdf from the shared box tests), draws the hit's RNG
-//      block (rng_top_up) and classifies the hit: miss, diffuse by the Mix coin
-//      (word 0 of that block: cosine / light), dielectric, metallic;
-//   C  a counting sort of the 256 slots by class (ballots + LDS prefix sums) deals
-//      each wave one class;
-//   D  every lane shades the slot it was dealt (segment_shade, unchanged), so the
-//      next rays of a wave are of one kind too (all toward the light, or all
-//      cosine-distributed): the next intersection is coherent as well;
-//   E  wave 0 commits finished rows in sample order (as path_kernel).
-// Each path's arithmetic and RNG words are path_kernel's: bit-identical images,
-// hit ids and counters (the parity suite's "sorted" form).
-constexpr int kSortW = RT_SORT_WAVES;      // waves per workgroup (render.h)
-constexpr int kSortN = kSortW * kWave;     // path slots per workgroup
-constexpr int kSortRing = 16;              // rows of the commit window (256 paths in flight)
-static_assert(kSortN == (int)kSortLanes && kSortRing == (int)kSortRingRows, "render.h sort_kernel constants");
-enum SortClass : uint32_t { kCMiss = 0, kCCos, kCLight, kCDiel, kCMetal, kCIdle, kNClass };
-// slot flags: bits 0-7 segments done (b), 8 busy, 9 pend, 10 inside, 11-13 class
-constexpr uint32_t kFBusy = 1u << 8, kFPend = 1u << 9, kFIn = 1u << 10;
-struct SortSlots {  // a workgroup's paths in LDS, [component][slot]
-    double o[3][kSortN], d[3][kSortN], T[3][kSortN], L[3][kSortN], n[3][kSortN];
-    double t[kSortN], pcos[kSortN];
-    uint64_t q0[kSortN], q1[kSortN];  // RNG block drawn at the hit (Rng::n0, n1)
-    uint32_t pix[kSortN], samp[kSortN], blk[kSortN], cur[kSortN], mat[kSortN], pmat[kSortN], flags[kSortN];
-};
-struct SortShared {  // workgroup-uniform stream state (path_kernel's wave-uniform scalars)
-    uint32_t base, next, open_end, uq_front, uq_back, drained;
-};
-RT_D V3 sl_get(const double (*a)[kSortN], uint32_t i) { return v3(a[0][i], a[1][i], a[2][i]); }
-RT_D void sl_put(double (*a)[kSortN], uint32_t i, V3 v) { a[0][i] = v.x; a[1][i] = v.y; a[2][i] = v.z; }
-
-template <bool ST, bool HIT>
-__global__ __launch_bounds__(kSortN, 3) void sort_kernel(const DevScene* __restrict__ Sg,
-                                                        const KParams* __restrict__ Pg, double* __restrict__ out,
-                                                        double* __restrict__ part, int32_t* __restrict__ hit_ids,
-                                                        unsigned long long* __restrict__ stats, uint32_t* spill_n,
-                                                        double* spill_t, uint32_t* __restrict__ queue,
-                                                        double* __restrict__ ring_all) {
-    __shared__ SortSlots sl;
-    __shared__ uint16_t perm[kSortN];               // lane -> slot (the last deal)
-    __shared__ uint32_t s_cls[kSortW][kNClass];     // per-wave class counts
-    __shared__ uint32_t s_idle[kSortW];
-    __shared__ uint32_t s_uq[kUQ * kUW];            // open wave-tiles (store_unit)
-    __shared__ uint32_t s_cnt[kSortRing];           // finished paths per ring row
-    __shared__ SortShared g;
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-    // no LDS stack: every push goes to the global spill area (sized for the deepest BVH;
-    // the Cornell-class scenes of this kernel push nothing: single-leaf BVHs)
-    auto stk = make_stack<false, 0>(nullptr, nullptr, 0u, (uint64_t)blockIdx.x * kSortN + wv * kWave, spill_n,
-                                    spill_t, gridDim.x * kSortN);
-    double* ring = ring_all + (uint64_t)blockIdx.x * kSortRing * kWave * 3;
-    const uint64_t below = (1ull << lane) - 1ull;
-    Cnt<ST> C;
-    C.zero();
-    perm[tid] = (uint16_t)tid;
-    sl.flags[tid] = 0u;
-    if (tid < kSortRing) s_cnt[tid] = 0u;
-    if (tid == 0) g = SortShared{0u, 0u, 0u, 0u, 0u, 0u};
-    V3 sum = v3(0.0, 0.0, 0.0);  // wave 0: the committed-row sums of its lane's pixel
-    uint32_t witers = 0;
-    __syncthreads();
-    for (;;) {
-        const DevScene& S = *opaque(Sg);
-        const KParams& P = *opaque(Pg);
-        const Scales sc{P.scale01, P.scale11};
-        const uint32_t depth = P.ray_depth;
-        const uint32_t n_units = P.n_slots * P.chunks * 4u;
-        // ---- A: idle slots take the next paths of the workgroup's row stream
-        uint32_t slot = perm[tid];
-        uint32_t fl = sl.flags[slot];
-        const bool idle = !(fl & kFBusy);
-        const uint64_t im = __ballot(idle);
-        if (lane == 0) s_idle[wv] = (uint32_t)__popcll(im);
-        __syncthreads();
-        uint32_t n_idle = 0;
-#pragma unroll
-        for (int w = 0; w < kSortW; ++w) n_idle += s_idle[w];
-        uint32_t before = 0;
-        for (uint32_t w = 0; w < wv; ++w) before += s_idle[w];
-        const uint32_t window = (g.base + kSortRing) * kWave;
-        if (tid == 0) {  // pull wave-tiles until the rows the idle slots could take exist
-            const uint32_t want = min(window, g.next + n_idle);
-            while (!g.drained && g.open_end * kWave < want && g.uq_back - g.uq_front < kUQ) {
-                const uint32_t unit = atomicAdd(queue, 1u);
-                if (unit >= n_units) { g.drained = 1u; break; }
-                const UnitGeo ug = unit_geo(P, unit);
-                store_unit(s_uq + (g.uq_back % kUQ) * kUW, g.open_end, ug);
-                g.open_end += ug.nrows;
-                ++g.uq_back;
-            }
-        }
-        __syncthreads();
-        const uint32_t next = g.next, limit = min(window, g.open_end * kWave), uq_back = g.uq_back;
-        if (idle) {
-            const uint32_t k = before + (uint32_t)__popcll(im & below);
-            if (next + k < limit) {
-                const uint32_t cur = next + k;
-                const uint32_t row = cur / kWave, col = cur % kWave;
-                const uint32_t* e = s_uq + unit_of_row(s_uq, uq_back, row) * kUW;
-                const uint32_t qxy = e[1];
-                const uint32_t px = (qxy & 0xFFFFu) + (col & 7u), py = (qxy >> 16) + (col >> 3);
-                const uint32_t smp = e[2] + (row - e[0]);
-                if ((e[5] & 1u) && px < P.width && py < P.height) {
-                    // Camera::fuzzy_ray + raytrace (camera.rs:48-55, raytrace.rs:8-10)
-                    const uint32_t pixel = py * P.width + px;
-                    Rng rng;
-                    rng_init(rng, P.seed, pixel, smp);
-                    const V3 dir = camera_dir(P, px, py, rng);  // block 0; afterwards {blk 1, nothing buffered}
-                    sl_put(sl.o, slot, load3(P.cam_pos));
-                    sl_put(sl.d, slot, dir);
-                    sl_put(sl.T, slot, v3(1.0, 1.0, 1.0));
-                    sl_put(sl.L, slot, v3(0.0, 0.0, 0.0));
-                    sl.pix[slot] = pixel; sl.samp[slot] = smp; sl.blk[slot] = rng.blk; sl.cur[slot] = cur;
-                    fl = kFBusy;
-                    C.path();
-                } else {
-                    atomicAdd(&s_cnt[row % kSortRing], 1u);  // no pixel: done at once, never read
-                }
-            }
-        }
-        // ---- B: the closest-hit query of every busy slot, then its branch class
-        uint32_t cls = kCIdle;
-        if (fl & kFBusy) {
-            C.step();
-            const uint32_t b = fl & 0xFFu;
-            const uint32_t pixel = sl.pix[slot], smp = sl.samp[slot];
-            if (b >= depth) {  // ray_depth 0: the path ends with no segment (raytrace.rs:9-11)
-                if (HIT) for (uint32_t k = b; k < depth; ++k) hit_ids[((uint64_t)pixel * P.spp + smp) * depth + k] = RT_HIT_NONE;
-                const uint32_t cur = sl.cur[slot];
-                double* rp = ring + ((uint64_t)((cur / kWave) % kSortRing) * kWave + cur % kWave) * 3;
-                const V3 L = sl_get(sl.L, slot);
-                rp[0] = L.x; rp[1] = L.y; rp[2] = L.z;
-                atomicAdd(&s_cnt[(cur / kWave) % kSortRing], 1u);
-                fl = 0u;
-            } else {
-                C.segment();
-                PathState ps;
-                ps.o = sl_get(sl.o, slot); ps.d = sl_get(sl.d, slot);
-                ps.pend = (fl & kFPend) != 0u;
-                Hit h; uint32_t mat = 0; int32_t gid = 0;
-                double impact = 0.0;
-                const bool hit = scene_intersect<ST, decltype(stk), true, kShapes>(S, ps.o, ps.d, stk, C, h, mat, gid,
-                                                                                 ps.pend, &impact);
-                if (ps.pend) {  // the previous bounce's Mix pdf and weight (raytrace.rs:26-33, ray_sampler.rs:95-97)
-                    const uint32_t nl = S.n_lights;
-                    const double lp = nl == 1u ? impact : impact / (double)nl;
-                    const double pdf = (sl.pcos[slot] + lp) / 2.0;
-                    const V3 w = diffuse_weight(load3(S.mats[sl.pmat[slot]].color), sl.pcos[slot], pdf);
-                    sl_put(sl.T, slot, mul(sl_get(sl.T, slot), w));
-                    fl &= ~kFPend;
-                }
-                if (HIT) hit_ids[((uint64_t)pixel * P.spp + smp) * depth + b] = hit ? gid : RT_HIT_MISS;
-                if (!hit) cls = kCMiss;
-                else {
-                    // segment_shade's first RNG steps, here: the next block is the coin's
-                    Rng rng;
-                    rng_init(rng, P.seed, pixel, smp);
-                    rng.blk = sl.blk[slot];
-                    rng_align(rng);
-                    rng_top_up(rng);
-                    sl.q0[slot] = rng.n0; sl.q1[slot] = rng.n1; sl.blk[slot] = rng.blk;
-                    const uint32_t kind = S.mats[mat].kind;
-                    if (kind == RT_MAT_DIFFUSE)
-                        cls = (S.n_lights == 0 || (uint32_t)rng.n0 < 0x80000000u) ? kCCos : kCLight;  // diffuse_draws' coin
-                    else cls = kind == RT_MAT_DIELECTRIC ? kCDiel : kCMetal;
-                    sl.t[slot] = h.t; sl_put(sl.n, slot, h.ns); sl.mat[slot] = mat;
-                    fl = h.inside ? (fl | kFIn) : (fl & ~kFIn);
-                }
-                fl = (fl & ~(7u << 11)) | (cls << 11);
-            }
-        }
-        sl.flags[slot] = fl;
-        // ---- C: deal the slots by class, each wave one class (a counting sort)
-        uint32_t rank = 0;
-#pragma unroll
-        for (uint32_t c = 0; c < kNClass; ++c) {
-            const uint64_t m = __ballot(cls == c);
-            if (lane == 0) s_cls[wv][c] = (uint32_t)__popcll(m);
-            if (cls == c) rank = (uint32_t)__popcll(m & below);
-        }
-        __syncthreads();
-        uint32_t pos = rank;
-        for (uint32_t c = 0; c < kNClass; ++c)
-            for (uint32_t w = 0; w < kSortW; ++w)
-                if (c < cls || (c == cls && w < wv)) pos += s_cls[w][c];
-        perm[pos] = (uint16_t)slot;
-        __syncthreads();
-        // ---- D: shade the dealt slot (segment_shade: the reference's shading, unchanged)
-        slot = perm[tid];
-        fl = sl.flags[slot];
-        cls = (fl >> 11) & 7u;
-        if ((fl & kFBusy) && cls != kCIdle) {
-            const uint32_t b = fl & 0xFFu;
-            const uint32_t pixel = sl.pix[slot], smp = sl.samp[slot];
-            PathState ps;
-            ps.o = sl_get(sl.o, slot); ps.d = sl_get(sl.d, slot);
-            ps.T = sl_get(sl.T, slot); ps.L = sl_get(sl.L, slot);
-            ps.pend = false;
-            Rng rng;
-            rng_init(rng, P.seed, pixel, smp);
-            bool hit = cls != kCMiss;
-            Hit h;
-            uint32_t mat = 0;
-            if (hit) {
-                rng.blk = sl.blk[slot]; rng.n0 = sl.q0[slot]; rng.n1 = sl.q1[slot]; rng.nready = 1u;
-                h.t = sl.t[slot]; h.ns = sl_get(sl.n, slot); h.ng = h.ns; h.inside = (fl & kFIn) != 0u;
-                mat = sl.mat[slot];
-            }
-            int32_t g_unused;
-            const bool more = b + 1 < depth;
-            const bool cont = segment_shade<ST, decltype(stk), true, kShapes>(S, P, sc, ps, rng, stk, C, hit, h, mat,
-                                                                              0, g_unused, more, !more);
-            const uint32_t nb = b + 1;
-            if (!cont || nb >= depth) {
-                if (HIT) for (uint32_t k = nb; k < depth; ++k) hit_ids[((uint64_t)pixel * P.spp + smp) * depth + k] = RT_HIT_NONE;
-                const uint32_t cur = sl.cur[slot];
-                double* rp = ring + ((uint64_t)((cur / kWave) % kSortRing) * kWave + cur % kWave) * 3;
-                rp[0] = ps.L.x; rp[1] = ps.L.y; rp[2] = ps.L.z;
-                atomicAdd(&s_cnt[(cur / kWave) % kSortRing], 1u);
-                fl = 0u;
-            } else {
-                rng_park(rng);
-                sl_put(sl.o, slot, ps.o); sl_put(sl.d, slot, ps.d);
-                sl_put(sl.T, slot, ps.T); sl_put(sl.L, slot, ps.L);
-                sl.blk[slot] = rng.blk;
-                if (ps.pend) { sl.pcos[slot] = ps.pcos; sl.pmat[slot] = ps.pmat; }
-                fl = kFBusy | (ps.pend ? kFPend : 0u) | nb;
-            }
-            sl.flags[slot] = fl;
-        }
-        ++witers;
-        if (tid == 0) g.next = min(limit, next + n_idle);
-        // the ring stores of this trip have reached the L2 before wave 0 reads them (past
-        // its L1) in the commit below
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        // ---- E: commit complete rows in stream order (wave 0: one lane per pixel of
-        // the wave-tile's 8x8 quadrant); the last row of the oldest open wave-tile writes
-        // its per-pixel sums (main.rs:104)
-        if (wv == 0) {
-            uint32_t base = g.base, uq_front = g.uq_front;
-            const uint32_t open_end = g.open_end;
-            while (base < open_end && s_cnt[base % kSortRing] == (uint32_t)kWave) {
-                // the row's entries were stored by any wave of the workgroup: read past the L1
-                double* rp = ring + ((uint64_t)(base % kSortRing) * kWave + lane) * 3;
-                const V3 v = v3(__hip_atomic_load(rp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                                __hip_atomic_load(rp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                                __hip_atomic_load(rp + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                sum = sum + v;
-                const uint32_t* e = s_uq + (uq_front % kUQ) * kUW;
-                if (base + 1u == e[0] + e[3]) {
-                    const uint32_t qxy = e[1], quad = e[5] >> 1;
-                    const uint32_t lx = (quad & 1u) * 8u + (lane & 7u), ly = (quad >> 1) * 8u + (lane >> 3);
-                    const bool own = (e[5] & 1u) && (qxy & 0xFFFFu) + (lane & 7u) < P.width &&
-                                     (qxy >> 16) + (lane >> 3) < P.height;
-                    const V3 res = own ? (P.chunks == 1 ? sum / (double)P.spp : sum) : v3(0.0, 0.0, 0.0);
-                    double* o = (P.chunks == 1 ? out : part) + ((uint64_t)e[4] * kBlock + ly * RT_TILE + lx) * 3;
-                    o[0] = res.x; o[1] = res.y; o[2] = res.z;
-                    sum = v3(0.0, 0.0, 0.0);
-                    ++uq_front;
-                }
-                __builtin_amdgcn_wave_barrier();
-                if (lane == 0) s_cnt[base % kSortRing] = 0u;
-                __builtin_amdgcn_wave_barrier();
-                ++base;
-            }
-            if (lane == 0) { g.base = base; g.uq_front = uq_front; }
-        }
-        __syncthreads();
-        if (g.drained && g.uq_front == g.uq_back) break;  // every pulled wave-tile written
-    }
-    wave_flush<ST>(C, stats, witers);
 }
 
 // trace_kernel — batch `intersect` (intersections.rs:42-62) as a persistent
@@ -2129,11 +1918,13 @@ PathFn path_fn_r(uint32_t waves, bool resume, int kinds) {
     if (kinds == kKindsCompact) return path_kernel<ST, HIT, RT_C3_W, true, kTris, true>;
 #else
     if (kinds == kKindsCompact) return path_kernel<ST, HIT, 4, true, kTris, true>;
+    if (kinds == kKindsCompact32) return path_kernel<ST, HIT, 4, true, kTris, true, true>;
 #endif
     return kinds == kTris ? path_kernel<ST, HIT, 4, true, kTris> : path_kernel<ST, HIT, 4, true>;
 #else
     if (waves == 4 && resume) {
         if (kinds == kKindsCompact) return path_kernel<ST, HIT, 4, true, kTris, true>;  // compact triangle layout
+        if (kinds == kKindsCompact32) return path_kernel<ST, HIT, 4, true, kTris, true, true>;  // + f32 decisions
         return kinds == kTris ? path_kernel<ST, HIT, 4, true, kTris> : path_kernel<ST, HIT, 4, true>;
     }
     kinds &= 3;  // the compact layout has only the triangle-only resumable instance (host: path_kinds)
@@ -2143,12 +1934,6 @@ PathFn path_fn_r(uint32_t waves, bool resume, int kinds) {
     return kinds == kShapes ? path_kernel<ST, HIT, 3, false, kShapes> : path_kernel<ST, HIT, 3, false>;
 #endif
 }
-using SortFn = void (*)(const DevScene*, const KParams*, double*, double*, int32_t*, unsigned long long*, uint32_t*,
-                       double*, uint32_t*, double*);
-SortFn sort_fn(bool stats, bool hits) {
-    if (stats) return hits ? sort_kernel<true, true> : sort_kernel<true, false>;
-    return hits ? sort_kernel<false, true> : sort_kernel<false, false>;
-}
 PathFn path_fn(bool stats, bool hits, uint32_t waves, bool resume, int kinds) {
     if (stats) return hits ? path_fn_r<true, true>(waves, resume, kinds) : path_fn_r<true, false>(waves, resume, kinds);
     return hits ? path_fn_r<false, true>(waves, resume, kinds) : path_fn_r<false, false>(waves, resume, kinds);
@@ -2156,16 +1941,13 @@ PathFn path_fn(bool stats, bool hits, uint32_t waves, bool resume, int kinds) {
 }  // namespace
 
 hipError_t path_grid(bool stats, bool hits, uint32_t waves, bool resume, int kinds, uint32_t n_units,
-                     uint32_t* grid, bool sorted) {
+                     uint32_t* grid) {
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e != hipSuccess) return e;
-    if (sorted)  // workgroups of kSortLanes: each pulls wave-tiles like a path_kernel wave
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)sort_fn(stats, hits), kSortN, 0);
-    else
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)path_fn(stats, hits, waves, resume, kinds),
-                                                         kWave, 0);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)path_fn(stats, hits, waves, resume, kinds),
+                                                     kWave, 0);
     if (e != hipSuccess) return e;
     const uint64_t g = (uint64_t)std::max(per_cu, 1) * (uint64_t)std::max(cus, 1);
     *grid = (uint32_t)std::min<uint64_t>(g, std::max<uint32_t>(n_units, 1u));
@@ -2185,13 +1967,9 @@ hipError_t launch_path(const DevScene& S, const KParams& P, const PathWork& W, d
     hipLaunchKernelGGL(stage_params_kernel, dim3(1), dim3(1), 0, st, W.d_params, P);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    if (W.sorted)
-        hipLaunchKernelGGL(sort_fn(stats != nullptr, hit_ids != nullptr), dim3(W.grid), dim3(kSortN), 0, st,
-                           W.d_scene, W.d_params, out, W.part, hit_ids, stats, W.spill_n, W.spill_t, W.queue, W.ring);
-    else
-        hipLaunchKernelGGL(path_fn(stats != nullptr, hit_ids != nullptr, W.waves, W.resume, W.kinds), dim3(W.grid),
-                           dim3(kWave), 0, st,
-                           S, P, W.d_scene, W.d_params, out, W.part, hit_ids, stats, W.spill_n, W.spill_t, W.queue, W.ring);
+    hipLaunchKernelGGL(path_fn(stats != nullptr, hit_ids != nullptr, W.waves, W.resume, W.kinds), dim3(W.grid),
+                       dim3(kWave), 0, st,
+                       S, P, W.d_scene, W.d_params, out, W.part, hit_ids, stats, W.spill_n, W.spill_t, W.queue, W.ring);
     e = hipGetLastError();
     if (e != hipSuccess || P.chunks == 1) return e;
     return launch_reduce_chunks(W.part, out, P, st);

@@ -133,6 +133,7 @@ struct DevBvh {
     // non-null only when every box coordinate and vertex is an exact f32
     const DevNodeC* cnodes;
     const float* ctris;
+    uint32_t c32;              // compact layout whose box coordinates are within 2^60 (rt_device.h Ray32)
 };
 
 struct DevScene {

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RT_API_VERSION 4
+#define RT_API_VERSION 5
 
 typedef enum rt_error {
     RT_OK = 0,
@@ -215,9 +215,12 @@ typedef struct rt_tuning {
     int32_t  compact;        /* -1 auto (1 when the scene has it: RT_LAYOUT_COMPACT_TRIS); 0 the f64
                                 triangle-BVH layout; 1 the compact one (triangle-only resumable kernel;
                                 RT_ERR_UNSUPPORTED on a scene without RT_LAYOUT_COMPACT_TRIS)           */
-    int32_t  sorted;         /* -1 auto; 1 the regrouped-shading kernel (shading dealt to the waves of a
-                                4-wave workgroup by branch class) for shape-only
-                                scenes on the fused segment form; 0 the one-wave kernel             */
+    int32_t  slab32;         /* -1 auto (1 on the compact layout); 1 the compact kernel decides each inner
+                                node's child tests in f32 under a proven error bound and runs the f64
+                                test only where the bound leaves a decision open (the f64 test's
+                                decisions either way); 0 every child test in f64.
+                                RT_ERR_UNSUPPORTED on a scene without RT_LAYOUT_COMPACT_TRIS
+                                (version 5: replaces version 4's `sorted`)                            */
 } rt_tuning;
 /* NULL restores every field to auto.  Fields out of range -> RT_ERR_INVALID. */
 int rt_scene_set_tuning(rt_scene* scene, const rt_tuning* tuning);

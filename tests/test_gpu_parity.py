@@ -34,7 +34,7 @@ def sink(rt, orc, scene_text):
 FORM = {}
 
 
-@pytest.fixture(autouse=True, params=["fused", "resume", "resume_eager", "resume_f64", "general", "sorted"])
+@pytest.fixture(autouse=True, params=["fused", "resume", "resume_eager", "resume_f64", "resume_slab64", "general"])
 def segment_form(request):
     """Every test runs both path-kernel segment forms: fused (whole closest-hit
     query, then shading) and resumable (triangle traversal suspended while few
@@ -45,20 +45,20 @@ def segment_form(request):
     "general" is the fused form in its all-kinds instance (kinds=3) where the
     host would pick a shape-only or triangle-only one (api.cpp path_kinds).
     The resumable forms read a glTF scene's triangle BVH in its compact layout
-    (f32 child boxes and vertices, exact copies: api.cpp path_compact);
-    "resume_f64" forces the f64 layout in the same kernel.
-    "sorted" runs shape-only scenes through the regrouped-shading kernel (render.hip
-    sort_kernel: paths in LDS slots of a 4-wave workgroup, shading dealt to the waves
-    by branch class); other scenes keep the fused one-wave kernel."""
+    (f32 child boxes and vertices, exact copies: api.cpp path_compact), whose
+    inner-node child tests are decided in f32 where a proven bound settles them
+    (rt_tuning.slab32, render.hip trav_step F32); "resume_slab64" runs every child
+    test of the compact layout in f64, "resume_f64" forces the f64 layout."""
     FORM.clear()
     FORM["resume"] = 1 if request.param.startswith("resume") else 0
     if request.param == "resume_eager":
         FORM.update(suspend_lanes=64, leaf_lanes=1)
     if request.param == "resume_f64":
         FORM["compact"] = 0
+    if request.param == "resume_slab64":
+        FORM["slab32"] = 0
     if request.param == "general":
         FORM["kinds"] = 3
-    FORM["sorted"] = 1 if request.param == "sorted" else 0
     yield request.param
     FORM.clear()
 
@@ -170,13 +170,12 @@ def test_dev_sqrt_matches_host(rt):
 def test_cornell_small(cornell, segment_form):
     desc, params, g, o = cornell
     _compare(g, o, params.replace(width=48, height=40, spp=4))
-    # shape-only on the fused form: the sorted form runs the regrouped kernel
-    assert g.tuning()["sorted"] == (1 if segment_form == "sorted" else 0)
+    # a shape-only scene has no compact triangle layout: no f32-decided child tests
+    assert g.tuning()["slab32"] == 0
 
 
-def test_sorted_wide_frame(cornell, segment_form):
-    """A frame with many wave-tiles per workgroup and long paths: the regrouped kernel's
-    workgroup stream (rows dealt to 256 slots, the 16-row commit window) in every form."""
+def test_wide_frame(cornell, segment_form):
+    """A frame with many wave-tiles per wave and long paths, in every form."""
     desc, params, g, o = cornell
     _compare(g, o, params.replace(width=96, height=64, spp=9, ray_depth=20, seed=5))
 
@@ -815,3 +814,55 @@ def test_fast_shape_edges(rt, orc):
     pd = np.concatenate([orig, dn], axis=1)
     assert np.array_equal(g.light_pdf(pd).view(np.uint64), o.light_pdf(pd).view(np.uint64))
     _compare(g, o, params)
+
+
+def deep_shape_scene_text(n_side=14, layers=10, seed=7):
+    """A shape-only scene with a few thousand rotated boxes and ellipsoids: shape BVHs
+    deep enough that closest-hit and light walks push many levels (advisor round 4: the
+    5-wave shape-only instance keeps no LDS stack, every push goes to the spill stack)."""
+    rng = np.random.default_rng(seed)
+    out = ["DIMENSIONS 64 48", "SAMPLES 3", "RAY_DEPTH 6", "BG_COLOR 0.1 0.12 0.15",
+           "CAMERA_POSITION 0.05 0.4 -4.2", "CAMERA_RIGHT 1 0 0", "CAMERA_UP 0 1 0", "CAMERA_FORWARD 0 -0.08 1",
+           "CAMERA_FOV_X 1.1", "", "NEW_PRIMITIVE", "PLANE 0 1 0", "POSITION 0 -1.2 0", "COLOR 0.6 0.6 0.6"]
+    for i in range(n_side):
+        for j in range(layers):
+            for k in range(n_side):
+                p = (np.array([i, j, k]) - np.array([n_side, layers, n_side]) / 2.0) * np.array([0.16, 0.18, 0.16])
+                p = p + rng.uniform(-0.03, 0.03, 3)
+                q = rng.standard_normal(4)
+                q /= np.linalg.norm(q)
+                kind = "BOX" if (i + j + k) % 2 == 0 else "ELLIPSOID"
+                s = rng.uniform(0.02, 0.06, 3)
+                out += ["", "NEW_PRIMITIVE", f"{kind} {float(s[0])!r} {float(s[1])!r} {float(s[2])!r}", f"POSITION {float(p[0])!r} {float(p[1])!r} {float(p[2])!r}",
+                        f"ROTATION {float(q[1])!r} {float(q[2])!r} {float(q[3])!r} {float(q[0])!r}"]
+                m = rng.integers(0, 10)
+                if m == 0:
+                    out.append("METALLIC")
+                elif m == 1:
+                    out.append("DIELECTRIC")
+                    out.append("IOR 1.4")
+                c = rng.uniform(0.2, 0.9, 3)
+                out.append(f"COLOR {float(c[0])!r} {float(c[1])!r} {float(c[2])!r}")
+    for x in (-0.7, 0.7):
+        out += ["", "NEW_PRIMITIVE", "BOX 0.3 0.02 0.3", f"POSITION {x} 1.4 0.2", "EMISSION 5 5 4"]
+    return "\n".join(out)
+
+
+@pytest.fixture(scope="module")
+def deep_shapes(rt, orc):
+    desc, params = rt.parse_scene(deep_shape_scene_text())
+    return desc, params, rt.Scene(desc), orc.OracleScene(desc)
+
+
+@pytest.mark.parametrize("waves", [3, 4, 5])
+def test_deep_shape_scene(deep_shapes, waves):
+    """Every register budget of the shape-only fused kernel on deep shape BVHs (the 4/5-wave
+    instances push every entry to the global spill stack, the 3-wave one keeps 12 in LDS) is
+    bit-exact; the host picks 3 waves for shape BVHs this large (api.cpp path_waves)."""
+    desc, params, g, o = deep_shapes
+    info = g.info()
+    assert max(info["bvh_depth"]) >= 10 and sum(info["bvh_nodes"]) > 64
+    g.set_tuning()
+    assert g.tuning()["waves"] == 3 and g.tuning()["kinds"] == 1 and g.tuning()["resume"] == 0
+    _, _, st = _compare(g, o, params, waves=waves, resume=0)
+    assert st["shape_tests"] > 0 and st["light_hits"] > 0
