@@ -398,7 +398,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc child passes (roofline=null)")
     ap.add_argument("--as-rank0-of", type=int, default=0, help=argparse.SUPPRESS)  # PMC child: rank 0's share
-    ap.add_argument("--tune", default="", help="experiments: force rt_tuning fields, e.g. slab32=0,waves=4 "
+    ap.add_argument("--tune", default="", help="experiments: force rt_tuning fields, e.g. compact=0,waves=4 "
                                                   "(the headline runs the library's own pick)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (RCCL over xGMI, the product path); gloo gathers host copies and lets several "

@@ -68,7 +68,7 @@ struct rt_scene {
     // bytes of the triangle BVH's compact layout (nodes + leaf blocks), 0 without one
     uint64_t compact_bytes = 0;
     // requested kernel form (rt_scene_set_tuning); auto fields resolve per scene
-    rt_tuning tune{0, -1, 0, 0, 0, 0, -1, -1};
+    rt_tuning tune{0, -1, 0, 0, 0, 0, -1};
 };
 
 namespace {
@@ -96,7 +96,6 @@ int upload_bvh(rt_scene* s, const HostBvhArrays& h, DevBvh& d) {
     d.depth = h.depth;
     d.fast = h.fast ? 1u : 0u;
     d.tri_q = h.tri_q ? 1u : 0u;
-    d.c32 = h.c32 ? 1u : 0u;
     if ((rc = upload(s, h.shapes, &d.shapes))) return rc;
     if ((rc = upload(s, h.tris, &d.tris))) return rc;
     if ((rc = upload(s, h.tri_cold, &d.tri_cold))) return rc;
@@ -318,13 +317,6 @@ bool path_compact(const rt_scene* s) {
     return s->tune.compact != 0 && s->dev.tris.cnodes && path_waves(s) == 4 && path_resume(s) && path_kinds(s) == 2;
 }
 
-// f32-decided child tests of the compact kernel (render.hip trav_step F32,
-// DESIGN.md §4): the same decisions as the f64 tests, made in f32 where a proven
-// bound settles them.  rt_tuning.slab32 forces it on (1) or off (0).
-bool path_slab32(const rt_scene* s) {
-    if (!path_compact(s) || !s->dev.tris.c32) return false;
-    return s->tune.slab32 >= 0 ? s->tune.slab32 == 1 : kSlab32Auto;
-}
 
 
 // Suspend threshold of the resumable traversal (render.h kSuspendCached /
@@ -361,7 +353,7 @@ int prepare_path(rt_scene* s, KParams& k, bool stats, bool hits, PathWork& W) {
     std::memset(&W, 0, sizeof(W));
     W.waves = path_waves(s);
     W.resume = path_resume(s);
-    W.kinds = path_compact(s) ? (path_slab32(s) ? kKindsCompact32 : kKindsCompact) : path_kinds(s);
+    W.kinds = path_compact(s) ? kKindsCompact : path_kinds(s);
     HIP_TRY(path_grid(stats, hits, W.waves, W.resume, W.kinds, (uint32_t)n_units, &W.grid));
     const uint64_t lanes = (uint64_t)W.grid * 64u;
     int rc;
@@ -624,7 +616,7 @@ int rt_scene_sample_chunks(const rt_scene* s, const rt_render_params* p, uint32_
 
 int rt_scene_set_tuning(rt_scene* s, const rt_tuning* t) {
     if (!s) return set_error(RT_ERR_INVALID, "scene is NULL");
-    if (!t) { s->tune = rt_tuning{0, -1, 0, 0, 0, 0, -1, -1}; return RT_OK; }
+    if (!t) { s->tune = rt_tuning{0, -1, 0, 0, 0, 0, -1}; return RT_OK; }
     if (t->waves != 0 && (t->waves < 3 || t->waves > 5)) return set_error(RT_ERR_INVALID, "waves must be 0, 3, 4 or 5");
     if (t->resume < -1 || t->resume > 1) return set_error(RT_ERR_INVALID, "resume must be -1, 0 or 1");
     if (t->kinds > 3) return set_error(RT_ERR_INVALID, "kinds must be 0..3");
@@ -635,9 +627,6 @@ int rt_scene_set_tuning(rt_scene* s, const rt_tuning* t) {
     if (t->compact < -1 || t->compact > 1) return set_error(RT_ERR_INVALID, "compact must be -1, 0 or 1");
     if (t->compact == 1 && !s->dev.tris.cnodes)
         return set_error(RT_ERR_UNSUPPORTED, "compact = 1: the scene has no compact triangle layout");
-    if (t->slab32 < -1 || t->slab32 > 1) return set_error(RT_ERR_INVALID, "slab32 must be -1, 0 or 1");
-    if (t->slab32 == 1 && !(s->dev.tris.cnodes && s->dev.tris.c32))
-        return set_error(RT_ERR_UNSUPPORTED, "slab32 = 1: the scene has no compact triangle layout within 2^60");
     s->tune = *t;
     return RT_OK;
 }
@@ -651,7 +640,6 @@ int rt_scene_get_tuning(const rt_scene* s, rt_tuning* out) {
     out->leaf_lanes = path_leaf_batch(s);
     out->chunk_spp = s->tune.chunk_spp;
     out->compact = path_compact(s) ? 1 : 0;
-    out->slab32 = path_slab32(s) ? 1 : 0;
     return RT_OK;
 }
 

@@ -69,8 +69,6 @@ inline void sample_chunks(uint32_t W, uint32_t H, uint32_t spp, uint32_t& chunks
 // compact layout (rt_layout.h DevNodeC): kTris | 4, only with the 4-wave
 // resumable instance (api.cpp path_kinds).
 constexpr int kKindsCompact = 6;
-constexpr int kKindsCompact32 = 14;  // kKindsCompact + f32-decided child tests (render.hip trav_step F32)
-constexpr bool kSlab32Auto = true;   // the host's pick for compact scenes (api.cpp path_slab32)
 
 // Device workspace of one path-kernel launch (owned by the scene).
 struct PathWork {

@@ -282,22 +282,9 @@ RT_D TriRec load_tri_c(const float* __restrict__ p) {
 // CMP: the triangle BVH's compact layout (DevBvh::cnodes / ctris, KIND 3 only):
 // the same boxes and vertices as exact f32 copies, widened to f64 before the
 // same arithmetic — every lane's visits, tests and results are the f64 form's.
-// F32 (compact layout only): the inner node's child tests are decided in f32
-// (rt_device.h slab32, Ray32 *R) and the f64 tests run only for lanes whose
-// decision the f32 bound leaves open — the f64 test's decisions either way.
-#ifndef RT_SLAB32_PAIR
-#define RT_SLAB32_PAIR 1
-#endif
-constexpr bool kSlabPair = RT_SLAB32_PAIR != 0;
-// f32 bounds on either side of the f64 best: blo <= best <= bhi
-RT_D void best32(double best, float& blo, float& bhi) {
-    const float b = (float)best;
-    blo = b * (1.0f - 0x1p-22f);
-    bhi = b * (1.0f + 0x1p-22f);
-}
-template <int KIND, int SLAB, bool ST, bool CMP = false, bool F32 = false, class Stk>
+template <int KIND, int SLAB, bool ST, bool CMP = false, class Stk>
 RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk& S, Cnt<ST>& C, Trav& T,
-                    uint64_t lv, int leaf_batch = kLeafBatch, const Ray32* R = nullptr) {
+                    uint64_t lv, int leaf_batch = kLeafBatch) {
     const unsigned long long ph_st = PH_T();
     const uint64_t at_leaf = __ballot(T.live && T.cnt != 0);
     const bool do_leaves = at_leaf == lv || __popcll(at_leaf) >= leaf_batch;
@@ -381,54 +368,20 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
         bool go_left = false, push = false;
         uint32_t pw = 0;
         double pt = 0.0;
-        bool exact = true;
-        if constexpr (F32) {
-            exact = !(R->E >= 0.0f);  // a ray that does not qualify: every test in f64
-            if (!exact) {
-                float vl, ml, vr, mr, blo, bhi;
-                bool zl, zr;
-                const int cl = slab32<kSlabPair>(w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, *R, vl, ml, zl);
-                const int cr = slab32<kSlabPair>(w1.z, w1.w, w2.x, w2.y, w2.z, w2.w, *R, vr, mr, zr);
-                best32(T.best, blo, bhi);
-                // v's interval (exactly 0 when z)
-                const float lhi = zl ? 0.0f : vl + ml, llo = zl ? 0.0f : vl - ml;
-                const float rhi = zr ? 0.0f : vr + mr, rlo = zr ? 0.0f : vr - mr;
-                // visit <=> hit && v < best (bvh.rs:161-165), decided either way or open
-                const bool lvis = cl == 1 && lhi < blo, lskip = cl == 0 || (cl == 1 && llo >= bhi);
-                const bool rvis = cr == 1 && rhi < blo, rskip = cr == 0 || (cr == 1 && rlo >= bhi);
-                exact = !(lvis || lskip) || !(rvis || rskip);
-                if (!exact) {
-                    if (lvis && rvis) {  // near first: left <=> v_l < v_r (bvh.rs:167)
-                        if (lhi < rlo) {
-                            push = true; pw = k.y; go_left = true;
-                            pt = zr ? 0.0 : stk_f32(vr, T.node, 1u);
-                        } else if (llo >= rhi) {
-                            push = true; pw = k.x;
-                            pt = zl ? 0.0 : stk_f32(vl, T.node, 0u);
-                        } else exact = true;
-                    } else if (lvis) go_left = true;
-                    else if (!rvis) next = true;
-                }
-                if (!exact) C.kids(cl == 1, cr == 1);
-            }
-        }
-        if (exact) {  // the f64 tests (bvh.rs:158-185)
-            double lt = 0.0, rt2 = 0.0;
-            const bool lh = slab_c<SLAB>(w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, o, d, rc, fast, lt);
-            const bool rh = slab_c<SLAB>(w1.z, w1.w, w2.x, w2.y, w2.z, w2.w, o, d, rc, fast, rt2);
-            C.kids(lh, rh);
-            const double bt = T.best;  // +inf when no hit yet
-            const double li = lh ? (lt < bt ? lt : bt) : bt;
-            const double ri = rh ? (rt2 < bt ? rt2 : bt) : bt;
-            if (li < bt) {
-                if (ri < bt) {
-                    push = true;
-                    // v >= 0 (or -0): + 0.0 clears the sign bit the f32 entries use (F32)
-                    if (li < ri) { pw = k.y; pt = ri + 0.0; go_left = true; }
-                    else { pw = k.x; pt = li + 0.0; }
-                } else go_left = true;
-            } else if (!(ri < bt)) next = true;
-        }
+        double lt = 0.0, rt2 = 0.0;
+        const bool lh = slab_c<SLAB>(w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, o, d, rc, fast, lt);
+        const bool rh = slab_c<SLAB>(w1.z, w1.w, w2.x, w2.y, w2.z, w2.w, o, d, rc, fast, rt2);
+        C.kids(lh, rh);
+        const double bt = T.best;  // +inf when no hit yet
+        const double li = lh ? (lt < bt ? lt : bt) : bt;
+        const double ri = rh ? (rt2 < bt ? rt2 : bt) : bt;
+        if (li < bt) {
+            if (ri < bt) {
+                push = true;
+                if (li < ri) { pw = k.y; pt = ri; go_left = true; }
+                else { pw = k.x; pt = li; }
+            } else go_left = true;
+        } else if (!(ri < bt)) next = true;
         if (push) S.push(pw, pt);
         if (!next) trav_enter<true>(B, T, go_left ? k.x : k.y);
         PH_ADD(kPhInnerCyc, ph_i);
@@ -467,23 +420,6 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
         while (S.sp > 0) {
             double tt;
             S.pop(w, tt);
-            if constexpr (F32) {
-                const int hw = __double2hiint(tt);
-                if (hw < 0) {  // an f32-decided entry (stk_f32): v' within eps v' + E
-                    const float v = __int_as_float(__double2loint(tt));
-                    const float m = fmaf(kEps32, v, R->E);
-                    float blo, bhi;
-                    best32(T.best, blo, bhi);
-                    if (v + m < blo) { found = true; break; }
-                    if (v - m >= bhi) continue;
-                    // open: the f64 test of that child, its box from the parent's line
-                    const float* bx = (const float*)(B.cnodes + (((uint32_t)hw >> 1) & 0x3FFFFFFFu)) + (hw & 1) * 6;
-                    double t = 0.0;
-                    (void)slab_c<SLAB>(bx[0], bx[1], bx[2], bx[3], bx[4], bx[5], o, d, rc, fast, t);
-                    if (t < T.best) { found = true; break; }
-                    continue;
-                }
-            }
             if (tt < T.best) { found = true; break; }
         }
         if (!found) T.live = false;
@@ -1150,21 +1086,19 @@ struct SegQuery {
     Cand best;
     Trav T;
     bool fast;  // unguarded slab division for the triangle BVH (DevBvh::fast && ray_fast)
-    Ray32 r32;  // the ray's f32 form for the f32-decided child tests (path_kernel F32)
 };
 
 // raytrace_impl's `intersect` call (raytrace.rs:13), first part: planes,
 // boxes and ellipsoids to completion, then the triangle traversal is set up.
 // KM == kTris (a triangle-only scene): no shapes to test, and the candidate is
 // the triangle traversal's alone (q.best is not carried across the loop)
-template <bool ST, int KM = 3, bool F32 = false, class Stk>
+template <bool ST, int KM = 3, class Stk>
 RT_D void segment_begin(const DevScene& S, const PathState& ps, Stk& stk, Cnt<ST>& C, SegQuery& q) {
     C.segment();
     q.rc = make_rcp3(ps.d);
     const bool rfast = ray_fast(ps.o, q.rc);
     if (KM != kTris) shapes_closest<ST, true>(S, ps.o, ps.d, q.rc, rfast, stk, C, q.best);
     q.fast = S.tris.fast && rfast;
-    if (F32) ray32_make(ps.o, ps.d, q.rc, q.fast && S.tris.c32, q.r32);
     trav_init<2, ST>(S.tris, ps.o, ps.d, q.rc, q.fast, stk, C, q.T);
 }
 
@@ -1498,7 +1432,7 @@ RT_D uint32_t unit_of_row(const uint32_t* uq, uint32_t uq_back, uint32_t row) {
 }
 
 
-template <bool ST, bool HIT, int WAVES, bool RES, int KM = 3, bool CMP = false, bool F32 = false>
+template <bool ST, bool HIT, int WAVES, bool RES, int KM = 3, bool CMP = false>
 __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams Pv,
                                                      const DevScene* __restrict__ Sg,
                                                      const KParams* __restrict__ Pg, double* __restrict__ out,
@@ -1655,7 +1589,7 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
             // lanes between segments (new paths, continued paths) start their query
             const unsigned long long ph_b = PH_T();
             if (busy && !inq && b < depth) {
-                segment_begin<ST, KM, F32>(S, ps, stk, C, q);
+                segment_begin<ST, KM>(S, ps, stk, C, q);
                 inq = true;
             }
             PH_ADDW(kPhIntersect, ph_b);
@@ -1672,8 +1606,7 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
                     const bool can_take = next < min(win, open_end * kWave) || (!drained && next < win);
                     if (__ballot((busy && !q.T.live) || (!busy && can_take))) break;
                 }
-                trav_step<3, 2, ST, CMP, F32>(S.tris, ps.o, ps.d, q.rc, q.fast, stk, C, q.T, lv, (int)P.leaf_batch,
-                                              &q.r32);
+                trav_step<3, 2, ST, CMP>(S.tris, ps.o, ps.d, q.rc, q.fast, stk, C, q.T, lv, (int)P.leaf_batch);
             }
             PH_ADD(kPhTris, ph_t);
             // lanes whose query finished shade and end (or continue) their segment
@@ -1918,13 +1851,11 @@ PathFn path_fn_r(uint32_t waves, bool resume, int kinds) {
     if (kinds == kKindsCompact) return path_kernel<ST, HIT, RT_C3_W, true, kTris, true>;
 #else
     if (kinds == kKindsCompact) return path_kernel<ST, HIT, 4, true, kTris, true>;
-    if (kinds == kKindsCompact32) return path_kernel<ST, HIT, 4, true, kTris, true, true>;
 #endif
     return kinds == kTris ? path_kernel<ST, HIT, 4, true, kTris> : path_kernel<ST, HIT, 4, true>;
 #else
     if (waves == 4 && resume) {
         if (kinds == kKindsCompact) return path_kernel<ST, HIT, 4, true, kTris, true>;  // compact triangle layout
-        if (kinds == kKindsCompact32) return path_kernel<ST, HIT, 4, true, kTris, true, true>;  // + f32 decisions
         return kinds == kTris ? path_kernel<ST, HIT, 4, true, kTris> : path_kernel<ST, HIT, 4, true>;
     }
     kinds &= 3;  // the compact layout has only the triangle-only resumable instance (host: path_kinds)

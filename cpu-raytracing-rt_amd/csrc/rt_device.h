@@ -402,90 +402,6 @@ RT_D bool aabb_hit(V3 mn, V3 mx, V3 o, V3 d, const Rcp3& rc, double& t) {
     return false;
 }
 
-// ---------------------------------------------- f32 child-box decisions ----
-// (round 5, DESIGN.md §4 "f32 child-box decisions").  The compact layout's boxes
-// are exact f32 values; an inner node's two child tests decide only comparisons
-// (hit or not, v < best, v_left < v_right, later v < best'), so they are made in
-// f32 with a proven bound on the distance to the f64 test's own quotients, and
-// the f64 test runs only for a lane whose decision the bound leaves open.  Every
-// lane therefore makes the f64 test's decisions: same visits, tests and results.
-//
-// Per ray: o = o32 + o_lo (o32 = RN32(o), o_lo = o - o32 exact in f64),
-// inv_k = RN32(dev_rcp(d_k)), oli_k = RN32(o_lo_k dev_rcp(d_k)); per plane b (an
-// exact f32 coordinate) q'_k = RN32(fma(RN32(b - o32_k), inv_k, -oli_k)).  With
-// q = (b - o_k) / d_k exact and q64 = RN(RN(b - o_k) / d_k) the f64 test's value,
-//   |q' - q| <= (2^-23 + 2^-24)(|q| + |o_lo_k / d_k|),  |q64 - q| <= 2^-52 |q|,
-// so |q' - q64| <= 2^-22.4 (|q'| + |oli_k|) to first order.  kEps32 = 2^-21 and
-// E = 2^-21 max_k |oli_k| + 2^-100 (2.7x slack: the second-order terms, the
-// roundings of the margins, f32 underflow) make eps |q'| + E a bound; a min or
-// max of such values keeps it for its result, so t_near', t_far' carry
-// M = eps max(|t_near'|, |t_far'|) + E.  Splitting o keeps the absolute term
-// 2^24 times smaller than RN32(o) would: a ray that leaves a surface EPSILON
-// above it resolves the faces through its origin (tools/f32slab_sim.c measured
-// the open decisions on the C3 / C5 scenes through the oracle's traversal).
-// A ray qualifies when |d_k| is in [2^-60, 2^60] and |o_k| <= 2^60 (no f32
-// overflow against boxes within 2^60, DevBvh::c32) and its f64 test is the
-// unguarded one (DevBvh::fast && ray_fast): hit <=> t_near <= t_far && t_far >= 0,
-// v = max(t_near, 0).  E < 0 marks a ray that does not (every test in f64).
-struct Ray32 {
-    float o[3], inv[3], oli[3];
-    float E;
-};
-constexpr float kEps32 = 0x1p-21f;
-RT_D bool r32_range(double x, int lo, int hi) {  // |x| in [2^lo, 2^hi]
-    const int e = (int)(((uint64_t)__double_as_longlong(x) >> 52) & 0x7ffu) - 1023;
-    return e >= lo && e < hi;
-}
-RT_D void ray32_make(V3 o, V3 d, const Rcp3& rc, bool fast, Ray32& R) {
-    const double ov[3] = {o.x, o.y, o.z}, rv[3] = {rc.r.x, rc.r.y, rc.r.z}, dv[3] = {d.x, d.y, d.z};
-    bool ok = fast;
-    float m = 0.0f;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        ok = ok && r32_range(dv[k], -60, 60) && fabs(ov[k]) <= 0x1p60;
-        R.o[k] = (float)ov[k];
-        R.inv[k] = (float)rv[k];
-        R.oli[k] = (float)((ov[k] - (double)R.o[k]) * rv[k]);
-        m = fmaxf(m, fabsf(R.oli[k]));
-    }
-    R.E = ok ? fmaf(kEps32, m, 0x1p-100f) : -1.0f;
-}
-// One child box in f32: 1 certain hit, 0 certain miss, 2 open (the f64 test
-// decides).  v = max(t_near', 0) within M of the f64 test's v; z: v is exactly 0
-// (t_near' + M <= 0, so the f64 t_near <= 0).  PAIR: the hit test compares only
-// pairs of different axes (x_k <= y_k holds on one axis exactly, so a flat box,
-// min = max on an axis, is decided too): D = min_j (y_j - max_{i != j} x_i).
-template <bool PAIR>
-RT_D int slab32(float lx, float ly, float lz, float hx, float hy, float hz, const Ray32& R, float& v, float& M,
-                bool& z) {
-    const float ax = fmaf(lx - R.o[0], R.inv[0], -R.oli[0]), bx = fmaf(hx - R.o[0], R.inv[0], -R.oli[0]);
-    const float ay = fmaf(ly - R.o[1], R.inv[1], -R.oli[1]), by = fmaf(hy - R.o[1], R.inv[1], -R.oli[1]);
-    const float az = fmaf(lz - R.o[2], R.inv[2], -R.oli[2]), bz = fmaf(hz - R.o[2], R.inv[2], -R.oli[2]);
-    const float x0 = fminf(ax, bx), x1 = fminf(ay, by), x2 = fminf(az, bz);
-    const float y0 = fmaxf(ax, bx), y1 = fmaxf(ay, by), y2 = fmaxf(az, bz);
-    const float tn = fmaxf(fmaxf(x0, x1), x2), tf = fminf(fminf(y0, y1), y2);
-    M = fmaf(kEps32, fmaxf(fabsf(tn), fabsf(tf)), R.E);
-    const float N = M + M;
-    const float D = PAIR ? fminf(fminf(y0 - fmaxf(x1, x2), y1 - fmaxf(x0, x2)), y2 - fmaxf(x0, x1)) : tf - tn;
-    v = fmaxf(tn, 0.0f);
-    z = tn + M <= 0.0f;
-#ifdef RT_SLAB32_UNSAFE  // experiment: no margins (not exact) — the f32 step's own speed
-    M = 0.0f; z = tn <= 0.0f;
-    return D >= 0.0f && tf >= 0.0f ? 1 : 0;
-#endif
-    if (D >= N && tf >= M) return 1;
-    if (D < -N || tf < -M) return 0;
-    return 2;
-}
-// A stack entry of the f32-decided form (render.hip trav_step): the 8-B t slot
-// holds either the f64 value (v >= 0, stored as v + 0 so the sign bit is clear) or
-// f32 v' in the low word and 1 | parent node (30 bits) | side in the high word;
-// the parent's line holds the child's box for the f64 test when a pop's decision
-// is open.
-RT_D double stk_f32(float v, uint32_t parent, uint32_t side) {
-    return __hiloint2double((int)(0x80000000u | (parent << 1) | side), __float_as_int(v));
-}
-
 // Quaternion::rotate_vector with an identity quaternion (s == 1, v == ±0):
 // every cross product term is a signed zero, so each NONZERO finite component
 // comes back bit-for-bit unchanged (x + ±0 == x).  Only a zero component can

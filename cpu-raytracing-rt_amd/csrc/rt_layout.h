@@ -55,9 +55,14 @@ inline uint32_t child_word(uint32_t node, uint32_t start, uint32_t count) {
 
 // Compact triangle-BVH node (DESIGN.md §2 "compact layout"): both children's
 // boxes as f32 — exact copies, the host checks that every coordinate of the
-// f64 boxes round-trips through f32 — plus the children's words (child_word).
-// 64 B instead of 128: a visit reads four 16-B words.  A leaf's entry keeps its
-// own range (read through a kLeafRef word).  Same node numbering as DevNode.
+// f64 boxes round-trips through f32 — plus the children's words.  64 B instead
+// of 128: a visit reads four 16-B words.  Slot order (scene_build.cpp
+// build_compact): the INTERNAL nodes in pre-order first (so an internal node's
+// internal left child is the next slot), then the few big leaves a child word
+// cannot pack.  A child word is an internal child's slot, a packed leaf
+// kPackedLeaf | count << 24 | leaf-block index (kLeafBlock, not a primitive
+// index), or a big leaf's slot | kLeafRef, whose entry holds its block index in
+// `start` and its primitive count in `count`.
 struct alignas(64) DevNodeC {
     float lmin[3], lmax[3], rmin[3], rmax[3];
     uint32_t lw, rw;            // child words of an internal node
@@ -133,7 +138,6 @@ struct DevBvh {
     // non-null only when every box coordinate and vertex is an exact f32
     const DevNodeC* cnodes;
     const float* ctris;
-    uint32_t c32;              // compact layout whose box coordinates are within 2^60 (rt_device.h Ray32)
 };
 
 struct DevScene {

@@ -406,9 +406,6 @@ void build_tri_bvh(const std::vector<TriItem>& items, HostBvhArrays& out, bool c
     HostBvh h = build_bvh(boxes);
     flatten(h, out);
     if (compact && !h.nodes.empty()) build_compact(h, items, out);
-    // every box lies in the root box: its coordinates bound all of them (rt_device.h Ray32)
-    auto in60 = [](V3 v) { return std::fabs(v.x) <= 0x1p60 && std::fabs(v.y) <= 0x1p60 && std::fabs(v.z) <= 0x1p60; };
-    out.c32 = !out.cnodes.empty() && in60(h.nodes[0].box.min) && in60(h.nodes[0].box.max);
     out.n_prims = (uint32_t)items.size();
     out.tris.reserve(items.size());
     // DevBvh::tri_q: the edges' range of the split-division triangle solve

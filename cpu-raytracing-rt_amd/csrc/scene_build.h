@@ -44,7 +44,6 @@ struct HostBvhArrays {
     uint32_t n_prims = 0, depth = 0;
     bool fast = false;  // all box coordinates pass coord_fast (DevBvh::fast)
     bool tri_q = false;  // every triangle edge component 0 or in [2^-149, 2^129) (DevBvh::tri_q)
-    bool c32 = false;    // a compact layout whose box coordinates are within 2^60 (DevBvh::c32)
     std::vector<DevShape> shapes;
     std::vector<DevTri> tris;
     std::vector<DevTriCold> tri_cold;

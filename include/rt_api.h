@@ -215,12 +215,9 @@ typedef struct rt_tuning {
     int32_t  compact;        /* -1 auto (1 when the scene has it: RT_LAYOUT_COMPACT_TRIS); 0 the f64
                                 triangle-BVH layout; 1 the compact one (triangle-only resumable kernel;
                                 RT_ERR_UNSUPPORTED on a scene without RT_LAYOUT_COMPACT_TRIS)           */
-    int32_t  slab32;         /* -1 auto (1 on the compact layout); 1 the compact kernel decides each inner
-                                node's child tests in f32 under a proven error bound and runs the f64
-                                test only where the bound leaves a decision open (the f64 test's
-                                decisions either way); 0 every child test in f64.
-                                RT_ERR_UNSUPPORTED on a scene without RT_LAYOUT_COMPACT_TRIS
-                                (version 5: replaces version 4's `sorted`)                            */
+    /* Version 5 removed version 4's last field (`sorted`, the regrouped-shading kernel).
+       Auto is 0 for the unsigned fields and -1 for the signed ones (resume, compact): a
+       zero-initialised struct is not all-auto.  NULL restores every field to auto. */
 } rt_tuning;
 /* NULL restores every field to auto.  Fields out of range -> RT_ERR_INVALID. */
 int rt_scene_set_tuning(rt_scene* scene, const rt_tuning* tuning);

@@ -49,8 +49,7 @@ def test_hairball(hairball, segment_form):
     assert st["tri_tests"] > 0 and st["shaded_hits"] > 0
     # glTF positions are f32: the compact triangle layout exists and the resumable forms read it
     assert g.info()["layout_flags"] & 1
-    assert g.tuning()["compact"] == (1 if segment_form in ("resume", "resume_eager", "resume_slab64") else 0)
-    assert g.tuning()["slab32"] == (1 if segment_form in ("resume", "resume_eager") else 0)
+    assert g.tuning()["compact"] == (1 if segment_form in ("resume", "resume_eager") else 0)
 
 
 def test_room(room):

@@ -34,7 +34,7 @@ def sink(rt, orc, scene_text):
 FORM = {}
 
 
-@pytest.fixture(autouse=True, params=["fused", "resume", "resume_eager", "resume_f64", "resume_slab64", "general"])
+@pytest.fixture(autouse=True, params=["fused", "resume", "resume_eager", "resume_f64", "general"])
 def segment_form(request):
     """Every test runs both path-kernel segment forms: fused (whole closest-hit
     query, then shading) and resumable (triangle traversal suspended while few
@@ -45,18 +45,14 @@ def segment_form(request):
     "general" is the fused form in its all-kinds instance (kinds=3) where the
     host would pick a shape-only or triangle-only one (api.cpp path_kinds).
     The resumable forms read a glTF scene's triangle BVH in its compact layout
-    (f32 child boxes and vertices, exact copies: api.cpp path_compact), whose
-    inner-node child tests are decided in f32 where a proven bound settles them
-    (rt_tuning.slab32, render.hip trav_step F32); "resume_slab64" runs every child
-    test of the compact layout in f64, "resume_f64" forces the f64 layout."""
+    (f32 child boxes and vertices, exact copies: api.cpp path_compact);
+    "resume_f64" forces the f64 layout in the same kernel."""
     FORM.clear()
     FORM["resume"] = 1 if request.param.startswith("resume") else 0
     if request.param == "resume_eager":
         FORM.update(suspend_lanes=64, leaf_lanes=1)
     if request.param == "resume_f64":
         FORM["compact"] = 0
-    if request.param == "resume_slab64":
-        FORM["slab32"] = 0
     if request.param == "general":
         FORM["kinds"] = 3
     yield request.param
@@ -170,8 +166,8 @@ def test_dev_sqrt_matches_host(rt):
 def test_cornell_small(cornell, segment_form):
     desc, params, g, o = cornell
     _compare(g, o, params.replace(width=48, height=40, spp=4))
-    # a shape-only scene has no compact triangle layout: no f32-decided child tests
-    assert g.tuning()["slab32"] == 0
+    # a shape-only scene has no compact triangle layout
+    assert g.tuning()["compact"] == 0
 
 
 def test_wide_frame(cornell, segment_form):
