@@ -112,14 +112,32 @@ PMC_PASSES = (
 )
 
 
-def class_prices(instance):
+def kernel_instance(tuning):
+    """The timed path-kernel instance's template arguments from the scene's resolved
+    form (rt_scene_get_tuning; render.hip path_fn_r): <ST, HIT, WAVES, RES, KM, CMP>."""
+    w, res, k = tuning["waves"], tuning["resume"] == 1, tuning["kinds"]
+    if res and w == 4:
+        km, cmp_ = (2, tuning["compact"] == 1) if k == 2 else (3, False)
+    elif res:
+        km, cmp_ = 3, False
+    else:
+        km, cmp_ = (1 if k == 1 else 3), False
+    return f"path_kernel<false, false, {w}, {'true' if res else 'false'}, {km}, {'true' if cmp_ else 'false'}>"
+
+
+def class_prices(kernel):
     """Static-mix mean prices of the int32 / cvt / f32 / rest classes for one kernel
-    instance (tools/valu_mix.py); None when the table is absent."""
+    instance (tools/valu_mix.py), matched by its template arguments; (None, None) when
+    the table has no row for that instance."""
     try:
-        d = json.load(open(PRICES_FILE))["instances"][instance]["classes"]
+        table = json.load(open(PRICES_FILE))["instances"]
     except (OSError, KeyError, ValueError):
-        return None
-    return {k: d[k]["mean_cycles"] for k in ("int32", "cvt", "f32", "rest") if k in d}
+        return None, None
+    for name, row in table.items():
+        if row.get("kernel") == kernel:
+            d = row["classes"]
+            return {k: d[k]["mean_cycles"] for k in ("int32", "cvt", "f32", "rest") if k in d}, name
+    return None, None
 
 
 DIST_ENV = ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
@@ -249,7 +267,8 @@ def valu_roofline(pmc, pmc_ns, kern_s, instance):
            pmc["SQ_INSTS_VALU_TRANS_F32"])
     rest = max(0.0, n - f64 - trans - i64 - i32 - cvt - f32)
     mix = {"int32": i32, "cvt": cvt, "f32": f32, "rest": rest}
-    prices = class_prices(instance) or {}
+    prices, row = class_prices(instance)
+    prices = prices or {}
     priced = {k: prices.get(k, (CHEAP + DEAR) / 2) for k in mix}
     fixed = VALU_CYCLES["f64"] * f64 + VALU_CYCLES["trans_f64"] * trans + VALU_CYCLES["int64"] * i64
     busy = fixed + sum(priced[k] * mix[k] for k in mix)  # SIMD issue cycles the launch needs
@@ -272,9 +291,11 @@ def valu_roofline(pmc, pmc_ns, kern_s, instance):
             "instr_per_launch": n, "f64_fma_mul_add": f64, "f64_trans": trans, "int64": i64, "int32": i32,
             "cvt": cvt, "f32": f32, "rest": rest,
             "issue_cycles_per_instr": {**VALU_CYCLES, **priced},
+            "kernel_instance": instance,
             "prices_source": ("profiles/r04/valu_rates_full.log (measured, 8 waves/SIMD); int32/cvt/f32/rest: "
-                              f"static-mix means of {instance} (tools/valu_prices.json)"
-                              if prices else "int32/cvt/f32/rest at the mid of the measured 32-bit range"),
+                              f"static-mix means of {instance} (tools/valu_prices.json row {row})"
+                              if prices else f"int32/cvt/f32/rest at the mid of the measured 32-bit range (no "
+                                             f"static-mix row for {instance})"),
             "busy_simd_cycles": busy,
             "frac_lower": lo / avail, "frac_upper": hi / avail,
             "clock_GHz": clk_used / 1e9, "clock_measured_GHz": clk / 1e9,
@@ -514,6 +535,19 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t
+    # the host copy of the frame's PPM payload (main.rs:74 writes it), outside the timed
+    # region: SURVEY §8d's end-to-end figure = ms_per_step + this D2H (pinned host buffer)
+    d2h_ms = None
+    if rank == 0 and part == world:
+        host_img = torch.empty(tuple(image.shape), dtype=torch.uint8, pin_memory=True)
+        d2h = []
+        for _ in range(3):
+            a = mark()
+            host_img.copy_(image, non_blocking=True)
+            b_ = mark()
+            b_.synchronize()
+            d2h.append(a.elapsed_time(b_))
+        d2h_ms = float(np.median(d2h))
     tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -555,8 +589,7 @@ def main():
             roofline = {"bound": "valu", "achieved": None, "peak": None, "unit": "G wave64 VALU instr/s",
                         "frac": None, "traffic": None, "note": f"PMC passes unavailable: {pmc_ns}"}
         else:
-            roofline = valu_roofline(pmc, pmc_ns, kern_s, "C2" if scene.tuning()["kinds"] == 1 else
-                                     ("C3" if scene.tuning()["compact"] == 1 else "tri_f64"))
+            roofline = valu_roofline(pmc, pmc_ns, kern_s, kernel_instance(scene.tuning()))
             traffic, detail = hbm_traffic(pmc)
             roofline["traffic"] = traffic
             roofline["hbm"] = {"achieved_GBps": traffic / kern_s / 1e9, "peak_GBps": HBM_PEAK_GBS,
@@ -615,7 +648,12 @@ def main():
             # 0's fused epilogue; max(render) / mean(render) is the render-side imbalance
             "phases_ms": {"render": per_rank[:, 0].tolist(), "gather": per_rank[:, 1].tolist(),
                           "epilogue": float(per_rank[0, 2]),
-                          "render_imbalance": float(per_rank[:, 0].max() / per_rank[:, 0].mean())},
+                          "render_imbalance": float(per_rank[:, 0].max() / per_rank[:, 0].mean()),
+                          # PPM payload device -> pinned host, median of 3, after the timed steps
+                          "d2h": d2h_ms},
+            # kernel-only (roofline.kernel_ms), whole step on the device (ms_per_step:
+            # render + gather + epilogue), and end to end with the payload's host copy
+            "end_to_end_ms_per_step": elapsed / args.steps * 1e3 + (d2h_ms or 0.0),
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(desc, params, args.cpu_seconds)

@@ -473,7 +473,8 @@ class Scene:
 
 class MultiScene:
     """generate_image over several GPUs of one process (rt_multi_*): one scene
-    replica per listed device (BVHs built once), the frame's tiles dealt
+    replica per listed device (BVHs built once, uploaded to devices[0] and
+    broadcast from there: ncclBroadcast, or peer copies), the frame's tiles dealt
     round-robin, one gather to devices[0] (RCCL ncclGather, or peer copies with
     peer=True, which also allows a device listed twice)."""
 
@@ -498,6 +499,20 @@ class MultiScene:
             self.close()
         except Exception:
             pass
+
+    def scene_info(self, index: int) -> dict:
+        """rt_scene_get_info of the replica on devices[index] (rt_multi_scene): devices[0]'s came
+        from the host, the others from devices[0] (ncclBroadcast / peer copies), whose fill time
+        is part of their upload_ms."""
+        h = lib().rt_multi_scene(self._h, index)
+        if not h:
+            raise IndexError(index)
+        i = rt_scene_info()
+        _check(lib().rt_scene_get_info(C.c_void_p(h), C.byref(i)))
+        out = {k: getattr(i, k) for k, _ in i._fields_}
+        out["bvh_nodes"] = list(i.bvh_nodes)
+        out["bvh_depth"] = list(i.bvh_depth)
+        return out
 
     def generate_image(self, params: RenderParams, ppm_bytes: bool = False, stats: bool = False):
         """(mean radiance [H, W, 3] f64, PPM payload [H, W, 3] u8 or None, stats dict)."""

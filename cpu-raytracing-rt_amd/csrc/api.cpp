@@ -44,6 +44,7 @@ struct rt_scene {
     int device = 0;
     DevScene dev{};
     std::vector<void*> allocs;
+    std::vector<size_t> alloc_bytes;  // bytes of each scene array in allocs (scene_allocs: replicas)
     rt_scene_info info{};
     // spill workspace for the traversal stack (grown on demand)
     uint32_t* spill_n = nullptr;
@@ -73,6 +74,11 @@ struct rt_scene {
 
 namespace {
 
+// Set while scene_upload builds a replica (multi.cpp): the arrays are allocated
+// but not copied from the host; the caller fills them device to device from the
+// source scene's arrays (the same build, so the same allocation sequence).
+thread_local bool g_replica = false;
+
 template <class T>
 int upload(rt_scene* s, const std::vector<T>& v, const T** out) {
     *out = nullptr;
@@ -80,7 +86,8 @@ int upload(rt_scene* s, const std::vector<T>& v, const T** out) {
     void* p = nullptr;
     HIP_TRY(hipMalloc(&p, v.size() * sizeof(T)));
     s->allocs.push_back(p);
-    HIP_TRY(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    s->alloc_bytes.push_back(v.size() * sizeof(T));
+    if (!g_replica) HIP_TRY(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
     s->info.device_bytes += v.size() * sizeof(T);
     *out = (const T*)p;
     return RT_OK;
@@ -485,7 +492,7 @@ int rt_scene_create(const rt_scene_desc* desc, rt_scene** out) {
     *out = nullptr;
     HostScene hs;
     const int rc = rt::scene_build_host(*desc, hs);
-    return rc ? rc : rt::scene_upload(hs, out);
+    return rc ? rc : rt::scene_upload(hs, out, false);
 }
 
 }  // extern "C"
@@ -501,8 +508,15 @@ int scene_build_host(const rt_scene_desc& desc, HostScene& hs) {
 }
 
 // Scene::new's device side: the flattened scene on the CURRENT HIP device.
-int scene_upload(const HostScene& hs, rt_scene** out) {
+// replica: allocate every scene array but copy none from the host (multi.cpp
+// fills them from devices[0]'s copy over xGMI, scene_allocs); the small records
+// (DevScene, stats) are still written here.
+int scene_upload(const HostScene& hs, rt_scene** out, bool replica) {
     *out = nullptr;
+    struct ReplicaFlag {
+        explicit ReplicaFlag(bool r) { g_replica = r; }
+        ~ReplicaFlag() { g_replica = false; }
+    } flag(replica);
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
         return set_error(RT_ERR_DEVICE, "no HIP device visible (the hot path has no CPU fallback)");
@@ -521,9 +535,12 @@ int scene_upload(const HostScene& hs, rt_scene** out) {
         (rc = upload_bvh(s, hs.bvh[4], d.lells)) || (rc = upload_bvh(s, hs.bvh[5], d.ltris)))
         return rc;
     // ellipsoid reciprocals for dev_quot: computed by the device's own rcp + Newton steps
-    HIP_TRY(launch_ell_rcp(const_cast<DevShape*>(d.ells.shapes), d.ells.n_prims, 0));
-    HIP_TRY(launch_ell_rcp(const_cast<DevShape*>(d.lells.shapes), d.lells.n_prims, 0));
-    HIP_TRY(hipStreamSynchronize(0));
+    // (a replica receives the source's records with them already written)
+    if (!replica) {
+        HIP_TRY(launch_ell_rcp(const_cast<DevShape*>(d.ells.shapes), d.ells.n_prims, 0));
+        HIP_TRY(launch_ell_rcp(const_cast<DevShape*>(d.lells.shapes), d.lells.n_prims, 0));
+        HIP_TRY(hipStreamSynchronize(0));
+    }
     {  // world normals of plane sides and box faces: rotated(Hit, rot) of render.hip materialise
         std::vector<double> pn(hs.planes.size() * 6), bn(hs.bvh[0].shapes.size() * 24, 0.0);
         for (size_t i = 0; i < hs.planes.size(); ++i) {
@@ -577,6 +594,12 @@ int scene_upload(const HostScene& hs, rt_scene** out) {
     *out = owner.release();
     return RT_OK;
 }
+
+const std::vector<void*>& scene_allocs(const rt_scene* s, const std::vector<size_t>** bytes) {
+    *bytes = &s->alloc_bytes;
+    return s->allocs;
+}
+void scene_add_upload_ms(rt_scene* s, double ms) { s->info.upload_ms += ms; }
 
 }  // namespace rt
 

@@ -19,7 +19,12 @@ struct HostScene;
 // records) and the upload of that build to the current HIP device, so a
 // multi-GPU frame (multi.cpp) builds once and uploads one replica per device.
 int scene_build_host(const rt_scene_desc& desc, HostScene& hs);
-int scene_upload(const HostScene& hs, rt_scene** out);
+int scene_upload(const HostScene& hs, rt_scene** out, bool replica);
+// A scene's device arrays in allocation order (with their sizes): a replica built
+// from the same HostScene allocates the same sequence, so array k of the replica
+// is filled from array k of the source (multi.cpp: ncclBroadcast or peer copies).
+const std::vector<void*>& scene_allocs(const rt_scene* s, const std::vector<size_t>** bytes);
+void scene_add_upload_ms(rt_scene* s, double ms);  // the replica's device-to-device fill time
 
 }  // namespace rt
 

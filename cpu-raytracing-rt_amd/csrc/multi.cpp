@@ -3,7 +3,10 @@
 // generate_image (main.rs:85-114) over the GPUs of one node from a single host
 // thread, so the Rust `main` (main.rs:73) keeps one call per frame:
 //   * the host builds the six BVHs once (scene.rs:180-223, bvh.rs:12-17) and
-//     every listed device gets its own replica of the flattened scene;
+//     uploads them to devices[0] only; every other listed device gets its
+//     replica from devices[0] over xGMI — one ncclBroadcast per scene array
+//     (peer copies under RT_MULTI_PEER) — instead of its own host copy (C5:
+//     ~1.7 GB per device over PCIe otherwise);
 //   * the frame's 16x16 tiles are dealt round-robin (tile t -> device index
 //     t % n), each device renders its share on its own stream
 //     (rt_render_tiles_async, the same partition torchrun ranks use);
@@ -50,6 +53,7 @@ struct Rccl {
     decltype(&ncclCommDestroy) comm_destroy = nullptr;
     decltype(&ncclCommAbort) comm_abort = nullptr;
     decltype(&ncclGather) gather = nullptr;
+    decltype(&ncclBroadcast) broadcast = nullptr;
     decltype(&ncclGroupStart) group_start = nullptr;
     decltype(&ncclGroupEnd) group_end = nullptr;
     decltype(&ncclGetErrorString) error_string = nullptr;
@@ -59,10 +63,12 @@ struct Rccl {
         comm_destroy = (decltype(comm_destroy))dlsym(h, "ncclCommDestroy");
         comm_abort = (decltype(comm_abort))dlsym(h, "ncclCommAbort");
         gather = (decltype(gather))dlsym(h, "ncclGather");
+        broadcast = (decltype(broadcast))dlsym(h, "ncclBroadcast");
         group_start = (decltype(group_start))dlsym(h, "ncclGroupStart");
         group_end = (decltype(group_end))dlsym(h, "ncclGroupEnd");
         error_string = (decltype(error_string))dlsym(h, "ncclGetErrorString");
-        if (!comm_init_all || !comm_destroy || !comm_abort || !gather || !group_start || !group_end || !error_string)
+        if (!comm_init_all || !comm_destroy || !comm_abort || !gather || !broadcast || !group_start || !group_end ||
+            !error_string)
             return false;
         handle = h;
         return true;
@@ -77,7 +83,7 @@ struct Rccl {
         for (const char* name : {"librccl.so.1", "/opt/rocm/lib/librccl.so.1"})
             if (void* h = dlopen(name, RTLD_NOW | RTLD_LOCAL))
                 if (bind(h)) return RT_OK;
-        return set_error(RT_ERR_UNSUPPORTED, "no RCCL with ncclGather/ncclCommInitAll found (librccl.so.1): "
+        return set_error(RT_ERR_UNSUPPORTED, "no RCCL with ncclGather/ncclBroadcast/ncclCommInitAll found (librccl.so.1): "
                                              "use RT_MULTI_PEER");
     }
 };
@@ -166,6 +172,57 @@ struct Drain {
     }
 };
 
+// The replicas' scene arrays from devices[0]'s (scene_upload's allocation order is
+// the build's, the same on every device): one ncclBroadcast per array, root 0, all
+// ranks in one group — over xGMI, devices[0]'s copy fans out without touching the
+// host — or, under RT_MULTI_PEER, one peer copy per array and replica.  The fill
+// time is added to each replica's rt_scene_info.upload_ms.
+int replicate_scene(rt_multi* m) {
+    const uint32_t n = (uint32_t)m->devs.size();
+    if (n < 2) return RT_OK;
+    const std::vector<size_t>* bytes0 = nullptr;
+    const std::vector<void*>& src = rt::scene_allocs(m->scenes[0], &bytes0);
+    std::vector<const std::vector<void*>*> dst(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        const std::vector<size_t>* b = nullptr;
+        dst[i] = &rt::scene_allocs(m->scenes[i], &b);
+        if (*b != *bytes0) return set_error(RT_ERR_DEVICE, "replica scene layout differs from devices[0]'s");
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    if (m->peer) {
+        for (uint32_t i = 1; i < n; ++i) {
+            MHIP(hipSetDevice(m->devs[i]));
+            for (size_t k = 0; k < src.size(); ++k)
+                MHIP(hipMemcpyPeerAsync((*dst[i])[k], m->devs[i], src[k], m->devs[0], (*bytes0)[k], m->streams[i]));
+        }
+    } else {
+        for (size_t k = 0; k < src.size(); ++k) {
+            ncclResult_t r = m->rccl.group_start();
+            for (uint32_t i = 0; i < n && r == ncclSuccess; ++i)
+                r = m->rccl.broadcast(src[k], i == 0 ? src[k] : (*dst[i])[k], (*bytes0)[k], ncclUint8, 0, m->comms[i],
+                                      m->streams[i]);
+            const ncclResult_t r2 = m->rccl.group_end();
+            if (r != ncclSuccess || r2 != ncclSuccess) {
+                for (ncclComm_t& c : m->comms)
+                    if (c) { (void)m->rccl.comm_abort(c); c = nullptr; }
+                m->comms_aborted = true;
+                for (uint32_t i = 0; i < n; ++i) {
+                    (void)hipSetDevice(m->devs[i]);
+                    (void)hipStreamSynchronize(m->streams[i]);
+                }
+                return set_error(RT_ERR_DEVICE, std::string("ncclBroadcast: ") + m->rccl.error_string(r ? r : r2));
+            }
+        }
+    }
+    for (uint32_t i = 0; i < n; ++i) {
+        MHIP(hipSetDevice(m->devs[i]));
+        MHIP(hipStreamSynchronize(m->streams[i]));
+    }
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    for (uint32_t i = 1; i < n; ++i) rt::scene_add_upload_ms(m->scenes[i], ms);
+    return RT_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -198,7 +255,8 @@ int rt_multi_create(const rt_scene_desc* desc, const int* devices, uint32_t n, u
         m->tiles.push_back(nullptr);
         m->tile_cap.push_back(0);
         MHIP(hipSetDevice(devices[i]));
-        if (int rc = rt::scene_upload(hs, &m->scenes[i])) return rc;
+        // devices[0] from the host; the others allocate only (filled below from devices[0])
+        if (int rc = rt::scene_upload(hs, &m->scenes[i], i > 0)) return rc;
         MHIP(hipStreamCreateWithFlags(&m->streams[i], hipStreamNonBlocking));
         MHIP(hipEventCreate(&m->ev0[i]));
         MHIP(hipEventCreate(&m->ev1[i]));
@@ -212,6 +270,7 @@ int rt_multi_create(const rt_scene_desc* desc, const int* devices, uint32_t n, u
             return set_error(RT_ERR_DEVICE, std::string("ncclCommInitAll: ") + m->rccl.error_string(r));
         }
     }
+    if (int rc = replicate_scene(m)) return rc;
     *out = owner.release();
     return RT_OK;
 }

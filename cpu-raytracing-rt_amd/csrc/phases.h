@@ -7,7 +7,7 @@ namespace rt {
 
 // ---- diagnostics: wave cycles per code region (tools/phases.py) ----------
 // Only in -DRT_PHASES builds: s_memtime deltas, added once per wave by the
-// first active lane into LDS, flushed to raw stats words 16..23 (kPhase*).
+// first active lane into LDS, flushed to raw stats words 16..16 + kPhN - 1 (16..50).
 // The last four words count BVH traversal-loop iterations (wave-level and
 // summed over lanes) and primitive tests (wave-level inner-loop trips and
 // lane-level tests): their ratios are the loop's SIMD utilisation.  Wave

@@ -66,10 +66,14 @@ struct Rng {
 // a ^ b ^ k in one gfx950 v_bitop3_b32 (truth table 0x96): the compiler emits two
 // v_xor_b32 for the chain, so a Philox round is 4 VALU instead of 6 (C2 -2.8%, C3
 // -0.5% at reduced spp, same digests; profiles/r04/variants_xor3_C*.log).  k is the
-// round key — the frame seed plus a round constant, wave-uniform (an SGPR operand).
+// round key — the frame seed plus a round constant — and MUST be wave-uniform: it is
+// the instruction's SGPR operand.  The readfirstlane states that (a per-lane key
+// would otherwise be read from the first active lane without notice); every key
+// comes from the frame's seed (rng_init / rng_rekey from KParams::seed), so it is
+// the value every lane holds, and the "s" constraint needs the same readfirstlane.
 RT_D uint32_t xor3(uint32_t a, uint32_t b, uint32_t k) {
     uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(__builtin_amdgcn_readfirstlane(k)));
     return r;
 }
 RT_D void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,

@@ -42,7 +42,7 @@ def test_valu_roofline_prices_every_class():
            "SQ_INSTS_VALU_INT32": 10.0, "SQ_INSTS_VALU_CVT": 5.0, "SQ_INSTS_VALU_ADD_F32": 0.0,
            "SQ_INSTS_VALU_MUL_F32": 0.0, "SQ_INSTS_VALU_FMA_F32": 0.0, "SQ_INSTS_VALU_TRANS_F32": 0.0,
            "SQ_THREAD_CYCLES_VALU": 3000.0, "SQ_ACTIVE_INST_VALU": 100.0, "GRBM_GUI_ACTIVE": 8 * 2.0e9 * 1e-6}
-    r = b.valu_roofline(pmc, 1000, 1e-6, "C2")
+    r = b.valu_roofline(pmc, 1000, 1e-6, "path_kernel<false, false, 5, false, 1, false>")
     d = r["valu_detail"]
     assert d["rest"] == 100 - 40 - 1 - 4 - 10 - 5
     assert d["frac_lower"] < r["frac"] < d["frac_upper"]
@@ -89,7 +89,22 @@ def test_f64_arith_frac():
            "SQ_INSTS_VALU_INT32": 10.0, "SQ_INSTS_VALU_CVT": 5.0, "SQ_INSTS_VALU_ADD_F32": 0.0,
            "SQ_INSTS_VALU_MUL_F32": 0.0, "SQ_INSTS_VALU_FMA_F32": 0.0, "SQ_INSTS_VALU_TRANS_F32": 0.0,
            "SQ_THREAD_CYCLES_VALU": 3000.0, "SQ_ACTIVE_INST_VALU": 100.0, "GRBM_GUI_ACTIVE": 8 * 2.0e9 * 1e-6}
-    d = b.valu_roofline(pmc, 1000, 1e-6, "C2")["valu_detail"]
+    d = b.valu_roofline(pmc, 1000, 1e-6, "path_kernel<false, false, 5, false, 1, false>")["valu_detail"]
     want = 40 * 30 / 1e-6 / (64 / 4.2 * 1024 * 2.0e9)
     assert abs(d["f64_arith_frac"] - want) < 1e-12 * want + 1e-18
     assert d["f64_instr_share"] == 0.4
+
+
+def test_kernel_instance_from_tuning():
+    """The VALU prices are the timed instance's own (render.hip path_fn_r's choice)."""
+    b = _bench()
+    c2 = dict(waves=5, resume=0, kinds=1, compact=0)
+    c3 = dict(waves=4, resume=1, kinds=2, compact=1)
+    f64 = dict(waves=4, resume=1, kinds=2, compact=0)
+    assert b.kernel_instance(c2) == "path_kernel<false, false, 5, false, 1, false>"
+    assert b.kernel_instance(c3) == "path_kernel<false, false, 4, true, 2, true>"
+    assert b.kernel_instance(f64) == "path_kernel<false, false, 4, true, 2, false>"
+    for t in (c2, c3, f64):
+        prices, row = b.class_prices(b.kernel_instance(t))
+        assert prices and row in ("C2", "C3", "tri_f64")
+    assert b.class_prices("path_kernel<false, false, 3, false, 3, false>") == (None, None)

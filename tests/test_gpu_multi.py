@@ -57,6 +57,23 @@ def test_peer_partition_matches_single(rt, cornell, n):
     m.close()
 
 
+def test_replicas_filled_from_device0(rt, cornell, atrium):
+    """devices[0] gets the scene from the host; every other replica is filled from it
+    device to device (rt_multi_create: ncclBroadcast, here peer copies), ellipsoid
+    reciprocals (written by devices[0]'s kernel) included: same layout, same bytes, and
+    the frames above are bit-identical; the fill is timed in the replica's upload_ms."""
+    for desc, params, ref, _ in (cornell, atrium):
+        m = rt.MultiScene(desc, [0, 0, 0], peer=True)
+        infos = [m.scene_info(i) for i in range(3)]
+        for i in (1, 2):
+            assert infos[i]["device_bytes"] == infos[0]["device_bytes"] > 0
+            assert infos[i]["bvh_nodes"] == infos[0]["bvh_nodes"]
+            assert infos[i]["upload_ms"] > 0.0
+        img, _, _ = m.generate_image(params)
+        assert np.array_equal(img, ref)
+        m.close()
+
+
 def test_peer_partition_triangles(rt, atrium):
     desc, params, ref, ref_st = atrium
     img, _, st = rt.MultiScene(desc, [0, 0, 0], peer=True).generate_image(params, stats=True)
