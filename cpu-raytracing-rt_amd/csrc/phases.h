@@ -21,7 +21,7 @@ enum { kPhAssign, kPhIntersect, kPhLightSample, kPhLightPdf, kPhSegment, kPhComm
        kPhPlanes = kPhW0 + 5, kPhBoxes, kPhElls, kPhTris, kPhMaterialise,
        kPhInnerWave, kPhInnerLane, kPhLiveLane, kPhRngFallWave, kPhRngFallLane,
        kPhPushLane, kPhPushGlobal, kPhPopGlobal, kPhLeafCyc, kPhInnerCyc, kPhPopCyc, kPhStepCyc, kPhN };  // traversal-stack pushes, past the LDS part
-static_assert(16 + kPhN <= 64, "phase words fit the raw stats");
+static_assert(16 + kPhN <= 52, "phase words fit the raw stats below the timeline words (render.h kTimeline)");
 constexpr int kPhW = kPhW0 - kPhIntersect;  // weighted word of region k = k + kPhW (k in 1..5)
 #ifdef RT_PHASES
 __shared__ unsigned long long g_phase[kPhN];

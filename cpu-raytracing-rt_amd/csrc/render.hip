@@ -1476,6 +1476,10 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
     // of the oldest open wave-tile writes that tile's sums.  Lanes never wait
     // for a wave-tile's longest path before starting the next one.
     const unsigned long long ph_tile = PH_T();
+    // stats instance: the wave's timeline (s_memrealtime, 100 MHz) — start, the trip
+    // that found the wave-tile queue drained, exit (raw stats words 52..59, tools/timeline.py)
+    const uint64_t tl_start = ST ? wall_clock64() : 0;
+    uint64_t tl_drain = 0;
     if (lane < kRing) s_cnt[lane] = 0;
     __syncthreads();
     V3 sum = v3(0.0, 0.0, 0.0);
@@ -1510,7 +1514,11 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
             uint32_t u = 0;
             if (lane == 0) u = atomicAdd(queue, 1u);
             const uint32_t unit = __builtin_amdgcn_readfirstlane(u);
-            if (unit >= n_units) { drained = true; break; }
+            if (unit >= n_units) {
+                drained = true;
+                if (ST) tl_drain = wall_clock64();
+                break;
+            }
             const UnitGeo g = unit_geo(Pt, unit);
             if (lane == 0) store_unit(s_uq + (uq_back % kUQ) * kUW, open_end, g);
             open_end += g.nrows;
@@ -1679,6 +1687,17 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
         if (drained && uq_front == uq_back) break;  // every pulled wave-tile written
     }
     wave_flush<ST>(C, stats, witers);
+    if (ST && lane == 0) {
+        const uint64_t te = wall_clock64(), td = tl_drain ? tl_drain : te;
+        atomicMax(&stats[kTimeline + 0], ~(unsigned long long)tl_start);  // ~ : earliest start
+        atomicMax(&stats[kTimeline + 1], (unsigned long long)te);         // last exit
+        atomicMax(&stats[kTimeline + 2], ~(unsigned long long)td);        // earliest drain
+        atomicMax(&stats[kTimeline + 3], (unsigned long long)td);         // last drain
+        atomicAdd(&stats[kTimeline + 4], (unsigned long long)(te - td));  // sum of drain-to-exit
+        atomicMax(&stats[kTimeline + 5], (unsigned long long)(te - td));
+        atomicAdd(&stats[kTimeline + 6], (unsigned long long)(te - tl_start));
+        atomicAdd(&stats[kTimeline + 7], 1ull);
+    }
     PH_ADD(kPhTile, ph_tile);
 #ifdef RT_PHASES
     if (ST && lane < kPhN) atomicAdd(&stats[kPhaseWord0 + lane], g_phase[lane]);

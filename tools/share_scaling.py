@@ -3,7 +3,8 @@ of an N-way partition (rt_render_tiles_async), timed alone with HIP events, for
 each N and EVERY rank (median of 3 timed runs after a warm one).  The slowest
 share x N over the N=1 frame is the render-side strong-scaling efficiency the
 N-GPU bench can reach (no gather or launch cost).
-usage: python tools/share_scaling.py [WORKLOAD] [SPP] [N ...]"""
+usage: python tools/share_scaling.py [WORKLOAD] [SPP] [N ...]
+RT_SHARE_TUNE="chunk_spp=4,..." forces rt_tuning fields (Scene.set_tuning)."""
 import json
 import os
 import sys
@@ -26,9 +27,12 @@ desc, params = bench.load_workload(rt, scene_file, W, H, spp)
 if depth:
     params = params.replace(ray_depth=depth)
 scene = rt.Scene(desc)
+tune = {k: int(v) for k, v in (kv.split("=", 1) for kv in os.environ.get("RT_SHARE_TUNE", "").split(",") if kv)}
+if tune:
+    scene.set_tuning(**tune)
 dev = torch.device("cuda", 0)
 stream = torch.cuda.current_stream(dev)
-out = {"workload": wl, "spp": spp, "chunks": rt.sample_chunks(params)[0], "ms": {}}
+out = {"workload": wl, "spp": spp, "chunks": scene.sample_chunks(params)[0], "tuning": scene.tuning(), "ms": {}}
 t1 = None
 for n in ns:
     per = scene.tiles_per_rank(params, n)
