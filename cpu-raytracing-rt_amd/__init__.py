@@ -105,10 +105,10 @@ class rt_scene_info(C.Structure):
 class rt_tuning(C.Structure):
     _fields_ = [("waves", C.c_uint32), ("resume", C.c_int32), ("kinds", C.c_uint32),
                 ("suspend_lanes", C.c_uint32), ("leaf_lanes", C.c_uint32), ("chunk_spp", C.c_uint32),
-                ("compact", C.c_int32)]
+                ("compact", C.c_int32), ("tail_split", C.c_uint32)]
 
 
-TUNING_AUTO = dict(waves=0, resume=-1, kinds=0, suspend_lanes=0, leaf_lanes=0, chunk_spp=0, compact=-1)
+TUNING_AUTO = dict(waves=0, resume=-1, kinds=0, suspend_lanes=0, leaf_lanes=0, chunk_spp=0, compact=-1, tail_split=0)
 RT_LAYOUT_COMPACT_TRIS = 0x1
 
 
@@ -381,7 +381,8 @@ class Scene:
     def set_tuning(self, **kw):
         """Force the kernel form of this scene's renders (rt_scene_set_tuning): waves (3|4|5; 5 = shape-only fused only),
         resume (0|1), kinds (3 = all-kinds instance), suspend_lanes, leaf_lanes (1..64),
-        chunk_spp, compact (0 = f64 triangle-BVH layout, 1 = compact when the scene has it).
+        chunk_spp, compact (0 = f64 triangle-BVH layout, 1 = compact when the scene has it),
+        tail_split (1 = every wave-tile whole, 2..8 = the queue's last wave-tiles in that many parts).
         Fields not given are auto (the library's per-scene pick)."""
         bad = set(kw) - set(TUNING_AUTO)
         if bad:

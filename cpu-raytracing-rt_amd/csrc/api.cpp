@@ -57,6 +57,9 @@ struct rt_scene {
     uint32_t* queue = nullptr;
     double* ring = nullptr;
     size_t ring_entries = 0;
+    // rows of the queue's split tail wave-tiles (KParams::rows), grown on demand
+    double* rows = nullptr;
+    size_t rows_entries = 0;
     unsigned long long* d_stats = nullptr;
     // the path kernel reads the scene record and the frame constants by pointer
     DevScene* d_scene = nullptr;
@@ -69,7 +72,7 @@ struct rt_scene {
     // bytes of the triangle BVH's compact layout (nodes + leaf blocks), 0 without one
     uint64_t compact_bytes = 0;
     // requested kernel form (rt_scene_set_tuning); auto fields resolve per scene
-    rt_tuning tune{0, -1, 0, 0, 0, 0, -1};
+    rt_tuning tune{0, -1, 0, 0, 0, 0, -1, 0};
 };
 
 namespace {
@@ -125,6 +128,7 @@ void free_scene(rt_scene* s) {
     if (s->part) (void)hipFree(s->part);
     if (s->queue) (void)hipFree(s->queue);
     if (s->ring) (void)hipFree(s->ring);
+    if (s->rows) (void)hipFree(s->rows);
     if (s->d_stats) (void)hipFree(s->d_stats);
     if (s->d_scene) (void)hipFree(s->d_scene);
     if (s->d_params) (void)hipFree(s->d_params);
@@ -376,6 +380,26 @@ int prepare_path(rt_scene* s, KParams& k, bool stats, bool hits, PathWork& W) {
         HIP_TRY(hipMalloc(&s->ring, ring_need * sizeof(double)));
         s->ring_entries = ring_need;
     }
+    // The queue's tail (render.hip queue_entry): the last wave-tiles — one
+    // per resident wave — handed out in kTailSplit parts, so the launch does not wait a
+    // whole wave-tile's time for the waves that took the last ones.  Capped at 256 MB of
+    // row buffer; rt_tuning.tail_split forces the split (1: whole wave-tiles).
+    const uint32_t split = s->tune.tail_split ? s->tune.tail_split : kTailSplit;
+    uint64_t tail = 0;
+    if (split > 1 && k.chunk_spp < (1u << 16)) {
+        const uint64_t per_unit = (uint64_t)k.chunk_spp * 64 * 3;  // doubles
+        tail = std::min<uint64_t>({n_units, (uint64_t)W.grid, (kTailRowBytes / 8) / per_unit});
+        if (tail * per_unit > s->rows_entries) {
+            if (int rc2 = ws_idle(s)) return rc2;
+            if (s->rows) (void)hipFree(s->rows);
+            s->rows = nullptr; s->rows_entries = 0;
+            HIP_TRY(hipMalloc(&s->rows, tail * per_unit * sizeof(double)));
+            s->rows_entries = tail * per_unit;
+        }
+    }
+    k.n_tail = (uint32_t)tail;
+    k.tail_split = tail ? split : 1u;
+    k.rows = s->rows;
     W.queue = s->queue; W.ring = s->ring; W.part = s->part;
     W.d_scene = s->d_scene; W.d_params = s->d_params;
     W.spill_n = s->spill_n; W.spill_t = s->spill_t;
@@ -639,7 +663,7 @@ int rt_scene_sample_chunks(const rt_scene* s, const rt_render_params* p, uint32_
 
 int rt_scene_set_tuning(rt_scene* s, const rt_tuning* t) {
     if (!s) return set_error(RT_ERR_INVALID, "scene is NULL");
-    if (!t) { s->tune = rt_tuning{0, -1, 0, 0, 0, 0, -1}; return RT_OK; }
+    if (!t) { s->tune = rt_tuning{0, -1, 0, 0, 0, 0, -1, 0}; return RT_OK; }
     if (t->waves != 0 && (t->waves < 3 || t->waves > 5)) return set_error(RT_ERR_INVALID, "waves must be 0, 3, 4 or 5");
     if (t->resume < -1 || t->resume > 1) return set_error(RT_ERR_INVALID, "resume must be -1, 0 or 1");
     if (t->kinds > 3) return set_error(RT_ERR_INVALID, "kinds must be 0..3");
@@ -650,6 +674,7 @@ int rt_scene_set_tuning(rt_scene* s, const rt_tuning* t) {
     if (t->compact < -1 || t->compact > 1) return set_error(RT_ERR_INVALID, "compact must be -1, 0 or 1");
     if (t->compact == 1 && !s->dev.tris.cnodes)
         return set_error(RT_ERR_UNSUPPORTED, "compact = 1: the scene has no compact triangle layout");
+    if (t->tail_split > 8) return set_error(RT_ERR_INVALID, "tail_split must be 0..8");
     s->tune = *t;
     return RT_OK;
 }
@@ -663,6 +688,7 @@ int rt_scene_get_tuning(const rt_scene* s, rt_tuning* out) {
     out->leaf_lanes = path_leaf_batch(s);
     out->chunk_spp = s->tune.chunk_spp;
     out->compact = path_compact(s) ? 1 : 0;
+    out->tail_split = s->tune.tail_split ? s->tune.tail_split : kTailSplit;
     return RT_OK;
 }
 

@@ -28,7 +28,10 @@ struct KParams {
     uint32_t n_slots;
     uint32_t suspend;     // live lanes below which the resumable kernel suspends traversal (api.cpp path_suspend)
     uint32_t leaf_batch;  // lanes waiting at leaves before the resumable kernel tests them (api.cpp path_suspend)
-    uint32_t _pad;
+    // the queue's last n_tail wave-tiles are handed out in tail_split parts whose rows
+    // go to `rows` ([n_tail][chunk_spp][64][3]); render.hip queue_entry / tail_combine_kernel
+    uint32_t n_tail, tail_split;
+    double* rows;
 };
 
 // device work counters: paths, segments, aabb, tri, shape, shaded, light queries,
@@ -105,6 +108,8 @@ constexpr uint32_t kSuspendCached = 32, kSuspendStreamed = 40;
 constexpr uint32_t kLeafCached = 32, kLeafStreamed = 24;
 constexpr uint64_t kCacheBytes = 256ull << 20;  // MI355X Infinity Cache (MALL)
 constexpr uint64_t kDeepSceneNodes = 4096;  // BVH nodes above which the 4-wave kernel runs
+constexpr uint32_t kTailSplit = 4;                      // parts per tail wave-tile (api.cpp prepare_path)
+constexpr uint64_t kTailRowBytes = 256ull << 20;        // row buffer cap of the split tail
 constexpr uint32_t kShapeWaves = 5;  // waves/SIMD of the shape-only fused kernel (api.cpp path_waves)
 constexpr uint64_t kShapeWavesNodes = 64;  // BVH nodes of a shape-only scene up to which it runs at kShapeWaves
 constexpr size_t kQueueWords = 16;  // wave-tile counter (word 0), padded to a 64-B line

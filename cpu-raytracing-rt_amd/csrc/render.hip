@@ -1417,12 +1417,36 @@ RT_D UnitGeo unit_geo(const KParams& P, uint32_t unit) {
     g.oslot = P.chunks == 1 ? slot : sci;  // out[slot] (means) or part[sci] (chunk sums)
     return g;
 }
+// The queue's tail (round 5, DESIGN.md §5 "per-launch tail"): the last P.n_tail
+// wave-tiles are handed out as P.tail_split parts of consecutive rows each, so the
+// waves that take the queue's last entries hold a fraction of a wave-tile when it
+// empties.  A part's rows go to the row buffer P.rows ([tail unit][row][lane][3]),
+// and tail_combine_kernel sums every tail wave-tile's rows in sample order after the
+// launch: the same additions in the same order as one wave's commit, so the frame
+// is bit-identical whatever the split (and for any rank count).  Queue entry q:
+// q < n_units - n_tail a whole wave-tile, else part (q - first) % split of tail
+// wave-tile (q - first) / split.  Returns false for an empty part.
+RT_D bool queue_entry(const KParams& P, uint32_t n_units, uint32_t q, UnitGeo& g, uint32_t& tail, uint32_t& roff) {
+    const uint32_t first = n_units - P.n_tail;
+    if (q < first) { g = unit_geo(P, q); tail = ~0u; roff = 0; return true; }
+    const uint32_t j = q - first, t = j / P.tail_split, part = j % P.tail_split;
+    g = unit_geo(P, first + t);
+    const uint32_t r0 = g.nrows * part / P.tail_split, r1 = g.nrows * (part + 1) / P.tail_split;
+    g.s0 += r0;
+    g.nrows = r1 - r0;
+    tail = t;
+    roff = r0;
+    return g.nrows > 0;
+}
 // an open wave-tile's LDS entry: first stream row, qx0 | qy0 << 16, first
-// sample, rows, output slot, tile_ok | quad << 1
+// sample, rows, output slot (a tail part: its tail unit), tile_ok | quad << 1
+// (| 8 | row offset in its wave-tile << 16 for a tail part)
 constexpr uint32_t kUQ = 8, kUW = 6;
-RT_D void store_unit(uint32_t* e, uint32_t first, const UnitGeo& g) {
-    e[0] = first; e[1] = g.qx0 | (g.qy0 << 16); e[2] = g.s0; e[3] = g.nrows; e[4] = g.oslot;
-    e[5] = (g.tile_ok ? 1u : 0u) | (g.quad << 1);
+constexpr uint32_t kUnitTail = 8u;
+RT_D void store_unit(uint32_t* e, uint32_t first, const UnitGeo& g, uint32_t tail = ~0u, uint32_t roff = 0) {
+    e[0] = first; e[1] = g.qx0 | (g.qy0 << 16); e[2] = g.s0; e[3] = g.nrows;
+    e[4] = tail == ~0u ? g.oslot : tail;
+    e[5] = (g.tile_ok ? 1u : 0u) | (g.quad << 1) | (tail == ~0u ? 0u : kUnitTail | (roff << 16));
 }
 // entry index of the open wave-tile holding stream row `row` (wave-uniform)
 RT_D uint32_t unit_of_row(const uint32_t* uq, uint32_t uq_back, uint32_t row) {
@@ -1463,6 +1487,7 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
     const KParams& Pt = WAVES == 3 ? *Pg : Pv;  // per-wave-tile constants
     const uint32_t depth = Pt.ray_depth;
     const uint32_t n_units = Pt.n_slots * Pt.chunks * 4u;
+    const uint32_t n_queue = n_units + Pt.n_tail * (Pt.tail_split - 1u);  // tail wave-tiles in parts
     Cnt<ST> C;
     C.zero();
 #ifdef RT_PHASES
@@ -1514,13 +1539,15 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
             uint32_t u = 0;
             if (lane == 0) u = atomicAdd(queue, 1u);
             const uint32_t unit = __builtin_amdgcn_readfirstlane(u);
-            if (unit >= n_units) {
+            if (unit >= n_queue) {
                 drained = true;
                 if (ST) tl_drain = wall_clock64();
                 break;
             }
-            const UnitGeo g = unit_geo(Pt, unit);
-            if (lane == 0) store_unit(s_uq + (uq_back % kUQ) * kUW, open_end, g);
+            UnitGeo g;
+            uint32_t tail, roff;
+            if (!queue_entry(Pt, n_units, unit, g, tail, roff)) continue;  // an empty tail part
+            if (lane == 0) store_unit(s_uq + (uq_back % kUQ) * kUW, open_end, g, tail, roff);
             open_end += g.nrows;
             ++uq_back;
             __syncthreads();
@@ -1665,12 +1692,19 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
         __syncthreads();
         while (base < open_end && s_cnt[base % kRing] == (uint32_t)kWave) {
             const double* rp = ring + ((uint64_t)(base % kRing) * kWave + lane) * 3;
-            sum = sum + v3(rp[0], rp[1], rp[2]);
+            const uint32_t* e = s_uq + (uq_front % kUQ) * kUW;
+            if (e[5] & kUnitTail) {  // a tail part: the row to the row buffer (tail_combine_kernel sums)
+                double* w = Pt.rows + (((uint64_t)e[4] * Pt.chunk_spp + (e[5] >> 16) + (base - e[0])) * kWave + lane) * 3;
+                w[0] = rp[0]; w[1] = rp[1]; w[2] = rp[2];
+            } else {
+                sum = sum + v3(rp[0], rp[1], rp[2]);
+            }
             __syncthreads();
             if (lane == 0) s_cnt[base % kRing] = 0;
             __syncthreads();
-            const uint32_t* e = s_uq + (uq_front % kUQ) * kUW;
-            if (base + 1u == e[0] + e[3]) {  // main.rs:104 for this wave-tile's pixels
+            if (base + 1u == e[0] + e[3] && (e[5] & kUnitTail)) {
+                ++uq_front;
+            } else if (base + 1u == e[0] + e[3]) {  // main.rs:104 for this wave-tile's pixels
                 const uint32_t qxy = e[1], quad = e[5] >> 1;
                 const uint32_t lx = (quad & 1u) * 8u + (lane & 7u), ly = (quad >> 1) * 8u + (lane >> 3);
                 const bool own = (e[5] & 1u) && (qxy & 0xFFFFu) + (lane & 7u) < Pt.width &&
@@ -1905,6 +1939,7 @@ hipError_t path_grid(bool stats, bool hits, uint32_t waves, bool resume, int kin
 }
 
 __global__ void stage_params_kernel(KParams* dst, KParams P) { *dst = P; }
+__global__ void tail_combine_kernel(KParams P, uint32_t n_units, double* __restrict__ out, double* __restrict__ part);
 
 hipError_t launch_path(const DevScene& S, const KParams& P, const PathWork& W, double* out, int32_t* hit_ids,
                        unsigned long long* stats, hipStream_t st) {
@@ -1921,8 +1956,31 @@ hipError_t launch_path(const DevScene& S, const KParams& P, const PathWork& W, d
                        dim3(kWave), 0, st,
                        S, P, W.d_scene, W.d_params, out, W.part, hit_ids, stats, W.spill_n, W.spill_t, W.queue, W.ring);
     e = hipGetLastError();
+    if (e == hipSuccess && P.n_tail) {
+        hipLaunchKernelGGL(tail_combine_kernel, dim3((P.n_tail + 3) / 4), dim3(4 * kWave), 0, st, P,
+                           P.n_slots * P.chunks * 4u, out, W.part);
+        e = hipGetLastError();
+    }
     if (e != hipSuccess || P.chunks == 1) return e;
     return launch_reduce_chunks(W.part, out, P, st);
+}
+
+// The queue's tail wave-tiles (queue_entry): each pixel's rows summed in sample order
+// from v3(0) — path_kernel's commit, addition for addition — and written where that
+// commit writes (means when chunks == 1, else the chunk partial).
+__global__ void tail_combine_kernel(KParams P, uint32_t n_units, double* __restrict__ out, double* __restrict__ part) {
+    const uint32_t lane = threadIdx.x & (kWave - 1), t = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+    if (t >= P.n_tail) return;
+    const UnitGeo g = unit_geo(P, n_units - P.n_tail + t);
+    const double* r = P.rows + ((uint64_t)t * P.chunk_spp * kWave + lane) * 3;
+    V3 sum = v3(0.0, 0.0, 0.0);
+    for (uint32_t k = 0; k < g.nrows; ++k) sum = sum + v3(r[(uint64_t)k * kWave * 3], r[(uint64_t)k * kWave * 3 + 1],
+                                                          r[(uint64_t)k * kWave * 3 + 2]);
+    const uint32_t lx = (g.quad & 1u) * 8u + (lane & 7u), ly = (g.quad >> 1) * 8u + (lane >> 3);
+    const bool own = g.tile_ok && g.qx0 + (lane & 7u) < P.width && g.qy0 + (lane >> 3) < P.height;
+    const V3 res = own ? (P.chunks == 1 ? sum / (double)P.spp : sum) : v3(0.0, 0.0, 0.0);
+    double* o = (P.chunks == 1 ? out : part) + ((uint64_t)g.oslot * kBlock + ly * RT_TILE + lx) * 3;
+    o[0] = res.x; o[1] = res.y; o[2] = res.z;
 }
 
 // Chunk partial sums -> per-pixel mean: ((p0 + p1) + ... + pK-1) / spp, in

@@ -215,9 +215,13 @@ typedef struct rt_tuning {
     int32_t  compact;        /* -1 auto (1 when the scene has it: RT_LAYOUT_COMPACT_TRIS); 0 the f64
                                 triangle-BVH layout; 1 the compact one (triangle-only resumable kernel;
                                 RT_ERR_UNSUPPORTED on a scene without RT_LAYOUT_COMPACT_TRIS)           */
-    /* Version 5 removed version 4's last field (`sorted`, the regrouped-shading kernel).
-       Auto is 0 for the unsigned fields and -1 for the signed ones (resume, compact): a
-       zero-initialised struct is not all-auto.  NULL restores every field to auto. */
+    uint32_t tail_split;     /* 0 auto (4); 1 every wave-tile whole; 2..8: the queue's last wave-tiles
+                                (one per resident wave) are handed out in this many parts of
+                                consecutive sample rows and summed in sample order after the launch
+                                (the same image: DESIGN.md section 5 "per-launch tail")            */
+    /* Version 5 replaced version 4's last field (`sorted`, the regrouped-shading kernel) with
+       tail_split.  Auto is 0 for the unsigned fields and -1 for the signed ones (resume,
+       compact): a zero-initialised struct is not all-auto.  NULL restores every field to auto. */
 } rt_tuning;
 /* NULL restores every field to auto.  Fields out of range -> RT_ERR_INVALID. */
 int rt_scene_set_tuning(rt_scene* scene, const rt_tuning* tuning);

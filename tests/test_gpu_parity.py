@@ -862,3 +862,25 @@ def test_deep_shape_scene(deep_shapes, waves):
     assert g.tuning()["waves"] == 3 and g.tuning()["kinds"] == 1 and g.tuning()["resume"] == 0
     _, _, st = _compare(g, o, params, waves=waves, resume=0)
     assert st["shape_tests"] > 0 and st["light_hits"] > 0
+
+
+@pytest.mark.parametrize("chunk_spp", [0, 1, 3])
+def test_tail_split_same_image(cornell, sink, chunk_spp):
+    """The queue's last wave-tiles handed out in parts (rt_tuning.tail_split, render.hip
+    queue_entry) and summed in sample order after the launch (tail_combine_kernel): the
+    image is bit-identical for every split, and the oracle's.  Small frames have fewer
+    wave-tiles than resident waves, so every wave-tile is a tail one here."""
+    for desc, params, g, o in (cornell, sink):
+        p = params.replace(width=40, height=24, spp=7, seed=9)
+        ref = None
+        for split in (1, 2, 3, 4, 8):
+            g.set_tuning(tail_split=split, chunk_spp=chunk_spp)
+            assert g.tuning()["tail_split"] == split
+            img, _, st = g.generate_image(p, stats=True)
+            if ref is None:
+                ref = img
+                _, cs = g.sample_chunks(p)
+                o_img, _, o_st = o.render(p, mode=1, chunk_spp=cs)
+                assert np.array_equal(img, o_img, equal_nan=True)
+            assert np.array_equal(img, ref, equal_nan=True), split
+        g.set_tuning()
