@@ -380,15 +380,17 @@ int prepare_path(rt_scene* s, KParams& k, bool stats, bool hits, PathWork& W) {
         HIP_TRY(hipMalloc(&s->ring, ring_need * sizeof(double)));
         s->ring_entries = ring_need;
     }
-    // The queue's tail (render.hip queue_entry): the last wave-tiles — one
-    // per resident wave — handed out in kTailSplit parts, so the launch does not wait a
-    // whole wave-tile's time for the waves that took the last ones.  Capped at 256 MB of
-    // row buffer; rt_tuning.tail_split forces the split (1: whole wave-tiles).
+    // The queue's tail (render.hip queue_entry): the last wave-tiles —
+    // kTailPerWave per resident wave, so a wave that took the last whole one finishes it
+    // while the others still take parts — handed out in kTailSplit parts, so the launch
+    // does not wait a whole wave-tile's time for the waves that took the last ones.
+    // Capped at 256 MB of row buffer; rt_tuning.tail_split forces the split (1: whole
+    // wave-tiles).
     const uint32_t split = s->tune.tail_split ? s->tune.tail_split : kTailSplit;
     uint64_t tail = 0;
     if (split > 1 && k.chunk_spp < (1u << 16)) {
         const uint64_t per_unit = (uint64_t)k.chunk_spp * 64 * 3;  // doubles
-        tail = std::min<uint64_t>({n_units, (uint64_t)W.grid, (kTailRowBytes / 8) / per_unit});
+        tail = std::min<uint64_t>({n_units, (uint64_t)W.grid * kTailPerWave, (kTailRowBytes / 8) / per_unit});
         if (tail * per_unit > s->rows_entries) {
             if (int rc2 = ws_idle(s)) return rc2;
             if (s->rows) (void)hipFree(s->rows);

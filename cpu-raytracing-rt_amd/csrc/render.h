@@ -108,7 +108,11 @@ constexpr uint32_t kSuspendCached = 32, kSuspendStreamed = 40;
 constexpr uint32_t kLeafCached = 32, kLeafStreamed = 24;
 constexpr uint64_t kCacheBytes = 256ull << 20;  // MI355X Infinity Cache (MALL)
 constexpr uint64_t kDeepSceneNodes = 4096;  // BVH nodes above which the 4-wave kernel runs
-constexpr uint32_t kTailSplit = 4;                      // parts per tail wave-tile (api.cpp prepare_path)
+constexpr uint32_t kTailSplit = 8;                      // parts per tail wave-tile (api.cpp prepare_path)
+#ifndef RT_TAIL_PER_WAVE
+#define RT_TAIL_PER_WAVE 3
+#endif
+constexpr uint64_t kTailPerWave = RT_TAIL_PER_WAVE;     // tail wave-tiles per resident wave
 constexpr uint64_t kTailRowBytes = 256ull << 20;        // row buffer cap of the split tail
 constexpr uint32_t kShapeWaves = 5;  // waves/SIMD of the shape-only fused kernel (api.cpp path_waves)
 constexpr uint64_t kShapeWavesNodes = 64;  // BVH nodes of a shape-only scene up to which it runs at kShapeWaves

@@ -215,8 +215,8 @@ typedef struct rt_tuning {
     int32_t  compact;        /* -1 auto (1 when the scene has it: RT_LAYOUT_COMPACT_TRIS); 0 the f64
                                 triangle-BVH layout; 1 the compact one (triangle-only resumable kernel;
                                 RT_ERR_UNSUPPORTED on a scene without RT_LAYOUT_COMPACT_TRIS)           */
-    uint32_t tail_split;     /* 0 auto (4); 1 every wave-tile whole; 2..8: the queue's last wave-tiles
-                                (one per resident wave) are handed out in this many parts of
+    uint32_t tail_split;     /* 0 auto (8); 1 every wave-tile whole; 2..8: the queue's last wave-tiles
+                                (three per resident wave) are handed out in this many parts of
                                 consecutive sample rows and summed in sample order after the launch
                                 (the same image: DESIGN.md section 5 "per-launch tail")            */
     /* Version 5 replaced version 4's last field (`sorted`, the regrouped-shading kernel) with
