@@ -7,7 +7,7 @@ namespace rt {
 
 // ---- diagnostics: wave cycles per code region (tools/phases.py) ----------
 // Only in -DRT_PHASES builds: s_memtime deltas, added once per wave by the
-// first active lane into LDS, flushed to raw stats words 16..16 + kPhN - 1 (16..50).
+// first active lane into LDS, flushed to raw stats words 16..16 + kPhN - 1 (16..51).
 // The last four words count BVH traversal-loop iterations (wave-level and
 // summed over lanes) and primitive tests (wave-level inner-loop trips and
 // lane-level tests): their ratios are the loop's SIMD utilisation.  Wave
@@ -15,12 +15,13 @@ namespace rt {
 // that test leaf primitives, kPhInnerCyc the inner-node visits, kPhPopCyc the
 // stack pops, kPhStepCyc whole steps (kPhTris minus it: the loop around them).
 // Regions timed with PH_ADDW also add cycles x (active lanes / 64) at k + kPhW:
-// the ratio of the two is the region's lane utilisation.
+// the ratio of the two is the region's lane utilisation.  kPhInnerUni counts the
+// compact inner-node wave steps whose lanes all visit the same node.
 enum { kPhAssign, kPhIntersect, kPhLightSample, kPhLightPdf, kPhSegment, kPhCommit, kPhTile,
        kPhTravWave, kPhTravLane, kPhLeafWave, kPhLeafLane, kPhRngWave, kPhRngLane, kPhW0,
        kPhPlanes = kPhW0 + 5, kPhBoxes, kPhElls, kPhTris, kPhMaterialise,
        kPhInnerWave, kPhInnerLane, kPhLiveLane, kPhRngFallWave, kPhRngFallLane,
-       kPhPushLane, kPhPushGlobal, kPhPopGlobal, kPhLeafCyc, kPhInnerCyc, kPhPopCyc, kPhStepCyc, kPhN };  // traversal-stack pushes, past the LDS part
+       kPhPushLane, kPhPushGlobal, kPhPopGlobal, kPhLeafCyc, kPhInnerCyc, kPhPopCyc, kPhStepCyc, kPhInnerUni, kPhN };  // traversal-stack pushes, past the LDS part
 static_assert(16 + kPhN <= 52, "phase words fit the raw stats below the timeline words (render.h kTimeline)");
 constexpr int kPhW = kPhW0 - kPhIntersect;  // weighted word of region k = k + kPhW (k in 1..5)
 #ifdef RT_PHASES

@@ -43,7 +43,7 @@ constexpr int kStatLqSkip = 10;  // raw word: last-bounce light queries the time
 // were hit by none / one / both of the two slab tests (stats instances only)
 constexpr int kStatKids0 = 11;
 constexpr int kTimeline = 52;     // stats path kernel: wave timeline words 52..59 (render.hip, tools/timeline.py)
-constexpr int kPhaseWord0 = 16;   // RT_PHASES builds: region cycles + loop counts at words 16..50 (16 + kPhN - 1)
+constexpr int kPhaseWord0 = 16;   // RT_PHASES builds: region cycles + loop counts at words 16..51 (16 + kPhN - 1)
 
 // Chunk count for a frame: a function of (W, H, spp) only, so the image does not
 // depend on the number of GPUs.  Doubles while the frame has < kChunkLanes

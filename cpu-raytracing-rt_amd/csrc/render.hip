@@ -364,6 +364,10 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
         const uint2 k = ((const uint2*)nw)[6];
         asm volatile("" ::"v"(w1.z), "v"(w1.w), "v"(w2.x), "v"(w2.y), "v"(w2.z), "v"(w2.w));  // see node_boxes
         PH_COUNT(kPhInnerWave, kPhInnerLane);
+#ifdef RT_PHASES
+        if (__ballot(T.node != (uint32_t)__builtin_amdgcn_readfirstlane(T.node)) == 0 && PH_FIRST())
+            atomicAdd(&g_phase[kPhInnerUni], 1ull);
+#endif
         C.aabb(2);
         bool go_left = false, push = false;
         uint32_t pw = 0;

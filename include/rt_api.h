@@ -258,7 +258,7 @@ int rt_render_tiles_async(rt_scene* scene, const rt_render_params* params,
    count the inner-node visits of closest-hit BVH traversals whose two child boxes
    were hit by none / one / both slab tests; builds compiled
    with -DRT_PHASES add wave cycles and loop counts per path-kernel region at
-   words 16..50 (16 + kPhN - 1, phases.h; tools/phases.py).  Not needed to render. */
+   words 16..51 (16 + kPhN - 1, phases.h; tools/phases.py).  Not needed to render. */
 int rt_read_raw_stats(rt_scene* scene, uint64_t* out, uint32_t n);
 
 /* Sample chunking of the work units: a pixel's spp samples are

@@ -22,7 +22,8 @@ NAMES = ["assign", "intersect", "light_sample", "light_pdf", "segment", "commit"
          "w_intersect", "w_light_sample", "w_light_pdf", "w_segment", "w_commit",
          "isect_planes", "isect_boxes", "isect_ellipsoids", "isect_triangles", "isect_materialise",
          "inner_wave_iters", "inner_lane_iters", "live_lane_iters", "rng_fallback_wave", "rng_fallback_lane",
-         "push_lane", "push_global", "pop_global", "leaf_cycles", "inner_cycles", "pop_cycles", "step_cycles"]
+         "push_lane", "push_global", "pop_global", "leaf_cycles", "inner_cycles", "pop_cycles", "step_cycles",
+         "inner_uniform_waves"]
 rt = load_package()
 wl = sys.argv[1]
 scene_file, W, H, spp, depth = bench.WORKLOADS[wl]
@@ -48,6 +49,7 @@ print(json.dumps({"workload": wl, "spp": spp, "segments": st["segments"],
                   "live_lane_frac": ph["live_lane_iters"] / max(1, 64 * ph["trav_wave_iters"]),
                   "inner_node_util": ph["inner_lane_iters"] / max(1, 64 * ph["inner_wave_iters"]),
                   "inner_iter_share": ph["inner_wave_iters"] / max(1, ph["trav_wave_iters"]),
+                  "inner_uniform_share": ph["inner_uniform_waves"] / max(1, ph["inner_wave_iters"]),
                   "leaf_loop_util": ph["leaf_lane_tests"] / max(1, 64 * ph["leaf_wave_trips"]),
                   "rng_refill_util": ph["rng_lane_refills"] / max(1, 64 * ph["rng_wave_refills"]),
                   "rng_wave_refills_per_segment": ph["rng_wave_refills"] * 64 / max(1, st["segments"]),
