@@ -188,6 +188,22 @@ def test_recursive_vs_iterative(rt, orc, scene_text, scene, over):
         assert sa[k] == sb[k]
 
 
+@pytest.mark.parametrize("seed", range(24))
+def test_recursive_vs_iterative_fuzz(rt, orc, seed):
+    """The two oracle forms on seeded random scenes (tests/fuzz_scenes.py): the same hit
+    ids and counters, radiance within reassociation."""
+    from fuzz_scenes import random_scene
+    desc, params = rt.parse_scene(random_scene(seed, spp=3))
+    o = orc.OracleScene(desc)
+    a, ha, sa = o.render(params, mode=0, hit_ids=True)
+    b, hb, sb = o.render(params, mode=1, hit_ids=True)
+    assert np.array_equal(ha, hb)
+    np.testing.assert_allclose(a, b, rtol=1e-12, atol=1e-300)
+    for k in ("paths", "segments", "aabb_tests", "tri_tests", "shape_tests", "shaded_hits",
+              "light_queries", "light_hits"):
+        assert sa[k] == sb[k]
+
+
 def _layout_z(o, params):
     """Per-pixel z of (the build's stream layout) - (the reference's literal rand call
     order): two independent estimates of each pixel's mean, sigma from the per-sample
