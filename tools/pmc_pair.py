@@ -14,7 +14,7 @@ def counters(d):
         for f in files:
             if f.endswith("counter_collection.csv"):
                 rows += [r for r in csv.DictReader(open(os.path.join(root, f)))
-                         if ("path_kernel<false" in r["Kernel_Name"] or "sort_kernel<false" in r["Kernel_Name"])]
+                         if "path_kernel<false" in r["Kernel_Name"]]
     last = max(int(r["Dispatch_Id"]) for r in rows)
     out = {}
     for r in rows:
