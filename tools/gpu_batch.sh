@@ -37,6 +37,8 @@ for s in $STEPS; do
              -- $B --workload C2 --steps 2 --warmup 1 --no-cpu-baseline --no-pmc || exit 1 ;;
     prof3) run prof_c3 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c3" -o run \
              -- $B --workload C3 --steps 2 --warmup 1 --no-cpu-baseline --no-pmc || exit 1 ;;
+    prof5) run prof_c5 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c5" -o run \
+             -- $B --workload C5 --steps 2 --warmup 1 --no-cpu-baseline --no-pmc || exit 1 ;;
     pmc2|pmc3)
       w=C${s#pmc}
       run fetch_$w 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch_$w" -o run \
