@@ -60,7 +60,10 @@ constexpr int kPhaseWord0 = 16;   // RT_PHASES builds: region cycles + loop coun
 constexpr uint64_t kChunkLanes = 8000000;
 constexpr uint32_t kMinChunkSpp = 8;
 constexpr uint32_t kMaxChunks = 64;
-constexpr uint64_t kPartBytes = 4ull << 30;
+#ifndef RT_PART_BYTES
+#define RT_PART_BYTES (4ull << 30)
+#endif
+constexpr uint64_t kPartBytes = RT_PART_BYTES;
 inline void sample_chunks(uint32_t W, uint32_t H, uint32_t spp, uint32_t& chunks, uint32_t& chunk_spp) {
     const uint64_t px = (uint64_t)W * H;
     const uint64_t chunk_bytes = (uint64_t)((W + 15) / 16) * ((H + 15) / 16) * 256 * 3 * sizeof(double);
