@@ -1445,7 +1445,13 @@ RT_D bool queue_entry(const KParams& P, uint32_t n_units, uint32_t q, UnitGeo& g
 // an open wave-tile's LDS entry: first stream row, qx0 | qy0 << 16, first
 // sample, rows, output slot (a tail part: its tail unit), tile_ok | quad << 1
 // (| 8 | row offset in its wave-tile << 16 for a tail part)
-constexpr uint32_t kUQ = 8, kUW = 6;
+// kUQ >= kRing: a split-tail part may hold a single row, and the resumable kernel's
+// suspend test counts the queue as able to feed idle lanes while the commit window
+// (kRing rows) is not yet open (can_take) — kUQ open wave-tiles must be able to cover
+// that window, or the wave spins without progress (an RT_RING_ROWS=16 build with
+// kUQ = 8 livelocked C5, round 5)
+constexpr uint32_t kUQ = (uint32_t)kRing > 8u ? (uint32_t)kRing : 8u, kUW = 6;
+static_assert(kUQ >= (uint32_t)kRing, "open wave-tiles must cover the commit window");
 constexpr uint32_t kUnitTail = 8u;
 RT_D void store_unit(uint32_t* e, uint32_t first, const UnitGeo& g, uint32_t tail = ~0u, uint32_t roff = 0) {
     e[0] = first; e[1] = g.qx0 | (g.qy0 << 16); e[2] = g.s0; e[3] = g.nrows;
