@@ -112,11 +112,14 @@ constexpr uint32_t kRingRows = RT_RING_ROWS;   // render.hip kRing (power of two
 // one that streams from HBM (C5, ~1.4 GB, past the 256-MiB Infinity Cache) at 40
 // (16: +16.6%, 24: +5.3%, 48: +1.6%; profiles/r02/variants/variants_suspend*.log):
 // there every lane sent back to issue its next ray adds memory-level parallelism.
-constexpr uint32_t kSuspendCached = 32, kSuspendStreamed = 40;
+// Round 5, with the 32-row commit window: streamed 40 -> 48 and its leaf batch
+// 24 -> 28, C5 196.7 -> 192.4 ms at 64 spp (56: 196.6, 64: 273; the cached pair
+// 32/32 still best on C3; profiles/r05/variants_knobs*_C*.log).
+constexpr uint32_t kSuspendCached = 32, kSuspendStreamed = 48;
 // Leaf batch of the same kernel (lanes waiting at leaves before the wave tests
 // them): C3 16 -> 32 lanes 236.3 -> 227.1 ms, C5 16 -> 24 lanes 260.3 -> 249.5 ms at
 // 64 spp (profiles/r02/variants/variants_leaflanes*.log).
-constexpr uint32_t kLeafCached = 32, kLeafStreamed = 24;
+constexpr uint32_t kLeafCached = 32, kLeafStreamed = 28;
 constexpr uint64_t kCacheBytes = 256ull << 20;  // MI355X Infinity Cache (MALL)
 constexpr uint64_t kDeepSceneNodes = 4096;  // BVH nodes above which the 4-wave kernel runs
 constexpr uint32_t kTailSplit = 8;                      // parts per tail wave-tile (api.cpp prepare_path)

@@ -3,7 +3,7 @@
 — the deep, HBM-streamed BVH (the triangle BVH and its records, ~0.7 GB in the
 compact layout, are past the 256-MiB Infinity Cache).
 
-Bar: the host picks the streamed-BVH form (suspend 40, leaf batch 24, compact
+Bar: the host picks the streamed-BVH form (suspend 48, leaf batch 28, compact
 layout: api.cpp bvh_streamed), the product instance's full frame is bit-identical
 to the stats instance's, and two full rows match the oracle's iterative form bit
 for bit with the device's sample chunking (bvh.rs:151-186 traversal in the
@@ -30,7 +30,7 @@ def test_c5_full_frame(rt, orc):
     assert info["layout_flags"] & 1  # f32 glTF positions: the compact triangle layout exists
     t = scene.tuning()
     assert (t["waves"], t["resume"], t["kinds"], t["compact"]) == (4, 1, 2, 1)
-    assert (t["suspend_lanes"], t["leaf_lanes"]) == (40, 24)  # streamed-BVH thresholds (render.h)
+    assert (t["suspend_lanes"], t["leaf_lanes"]) == (48, 28)  # streamed-BVH thresholds (render.h)
     chunks, chunk_spp = scene.sample_chunks(params)
 
     img, _, st = scene.generate_image(params, stats=True)     # stats instance
