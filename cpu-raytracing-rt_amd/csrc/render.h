@@ -89,18 +89,20 @@ struct PathWork {
     int kinds;            // the scene's primitive kinds, kShapes 1 | kTris 2 (path_kernel KM); kKindsCompact
     uint32_t grid;        // persistent waves (path_grid)
     uint32_t* queue;      // wave-tile counter, zeroed by launch_path
-    double* ring;         // [grid][kRing=32][64][3] finished-path radiance
+    double* ring;         // [grid][kRing=64][64][3] finished-path radiance
     double* part;         // [n_slots*chunks][256][3] chunk partial sums (chunks > 1)
     uint32_t* spill_n;    // traversal-stack spill, stride grid*64
     double* spill_t;
 };
-// Rows of a wave's commit window (round 5: 32, was 8).  A path still running in
+// Rows of a wave's commit window (round 5: 64, was 8).  A path still running in
 // the oldest open row holds the window; the resumable kernel's lanes then idle once
-// the window's paths are all taken.  C5 -4.9% (207.3 -> 197.0 ms at 64 spp), C3
-// -0.7%, C2 +0.1%; 64 rows lose (the 4-wave kernel's LDS no longer fits 16 waves a
-// CU: C5 212 ms, C3 +8%) (profiles/r05/variants_ring*_C*.log).
+// the window's paths are all taken.  32 rows: C5 -4.9% (207.3 -> 197.0 ms at 64 spp),
+// C3 -0.7%, C2 +0.1%.  64 rows lost at first (C5 212 ms, C3 +8%: with 64 open
+// wave-tile entries the 4-wave kernel's LDS no longer fit 16 waves a CU); with 16
+// entries (render.hip kUQ) it fits and gains again: C5 -1.6%, C3 -0.3%
+// (profiles/r05/variants_ring*_C*.log, variants_u16_C*.log).
 #ifndef RT_RING_ROWS
-#define RT_RING_ROWS 32
+#define RT_RING_ROWS 64
 #endif
 constexpr uint32_t kRingRows = RT_RING_ROWS;   // render.hip kRing (power of two, <= 64)
 // Suspend threshold of the resumable triangle traversal (path_kernel RES): fewer

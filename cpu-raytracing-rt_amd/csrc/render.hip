@@ -1445,13 +1445,17 @@ RT_D bool queue_entry(const KParams& P, uint32_t n_units, uint32_t q, UnitGeo& g
 // an open wave-tile's LDS entry: first stream row, qx0 | qy0 << 16, first
 // sample, rows, output slot (a tail part: its tail unit), tile_ok | quad << 1
 // (| 8 | row offset in its wave-tile << 16 for a tail part)
-// kUQ >= kRing: a split-tail part may hold a single row, and the resumable kernel's
-// suspend test counts the queue as able to feed idle lanes while the commit window
-// (kRing rows) is not yet open (can_take) — kUQ open wave-tiles must be able to cover
-// that window, or the wave spins without progress (an RT_RING_ROWS=16 build with
-// kUQ = 8 livelocked C5, round 5)
-constexpr uint32_t kUQ = (uint32_t)kRing > 8u ? (uint32_t)kRing : 8u, kUW = 6;
-static_assert(kUQ >= (uint32_t)kRing, "open wave-tiles must cover the commit window");
+// Open wave-tiles a wave may hold (s_uq).  A split-tail part may hold a single row,
+// so kUQ of them can cover fewer rows than the commit window (kRing); the resumable
+// kernel's suspend test therefore counts the queue as able to feed idle lanes only
+// while another wave-tile can be opened (can_take) — without that condition an
+// RT_RING_ROWS=16 build with kUQ = 8 spun without progress on C5 (round 5).
+// 16 entries: 384 B of LDS (the 64-row window with 64 entries pushed the 4-wave
+// kernel past 16 waves a CU); 16 whole wave-tiles of >= 8 rows cover the window.
+#ifndef RT_OPEN_UNITS
+#define RT_OPEN_UNITS 16
+#endif
+constexpr uint32_t kUQ = RT_OPEN_UNITS, kUW = 6;
 constexpr uint32_t kUnitTail = 8u;
 RT_D void store_unit(uint32_t* e, uint32_t first, const UnitGeo& g, uint32_t tail = ~0u, uint32_t roff = 0) {
     e[0] = first; e[1] = g.qx0 | (g.qy0 << 16); e[2] = g.s0; e[3] = g.nrows;
@@ -1648,7 +1652,8 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
                 if (lv == 0) break;
                 if (__popcll(lv) < (int)P.suspend) {
                     const uint32_t win = (base + kRing) * kWave;
-                    const bool can_take = next < min(win, open_end * kWave) || (!drained && next < win);
+                    const bool can_take = next < min(win, open_end * kWave) ||
+                                          (!drained && next < win && uq_back - uq_front < kUQ);
                     if (__ballot((busy && !q.T.live) || (!busy && can_take))) break;
                 }
                 trav_step<3, 2, ST, CMP>(S.tris, ps.o, ps.d, q.rc, q.fast, stk, C, q.T, lv, (int)P.leaf_batch);
