@@ -53,11 +53,10 @@ constexpr int kPhaseWord0 = 16;   // RT_PHASES builds: region cycles + loop coun
 // kMaxChunks, and by kPartBytes: the chunk partial sums ([tiles][chunks][256][3]
 // f64, written and reduced once per frame) stay within 4 GiB over all ranks
 // (C2/C3: 32 chunks, 1.6 GB; C4 3840x2160: 16 chunks, 3.2 GB — 64 would be
-// 12.7 GB); then trimmed so no chunk is empty.  kChunkLanes was 32M until round 5,
-// which cut C5 (1920x1080, 64 spp) to 4-spp chunks; 8M gives it 8-spp chunks, 4.5%
-// faster (206-208 vs 215-219 ms; 12- and 16-spp chunks time the same, 32 and 64
-// are slower: profiles/r05/variants_chunk*_C5.log) and leaves C1-C4 as they were.
-constexpr uint64_t kChunkLanes = 8000000;
+// 12.7 GB); then trimmed so no chunk is empty.  (Round 5 tried 8M runs, which gave C5
+// 8-spp chunks: 4.5% faster with the 8-row commit window, but 1.5% slower than these
+// 4-spp chunks once the window is 64 rows, so 32M stays: profiles/r05/variants_chunk*_C5.log.)
+constexpr uint64_t kChunkLanes = 32000000;
 constexpr uint32_t kMinChunkSpp = 8;
 constexpr uint32_t kMaxChunks = 64;
 #ifndef RT_PART_BYTES

@@ -264,11 +264,11 @@ def test_chunked_sum_is_reassociation_only(rt, orc, scene_text):
 @pytest.mark.parametrize("w,h,spp,want", [
     (1920, 1080, 256, (32, 8)),     # C2/C3: 8-spp chunks (66M work units: short wave-tiles trim the 8-GPU tail)
     (3840, 2160, 1024, (16, 64)),   # C4: capped by the 4-GiB partial-sum budget (64 chunks: 12.7 GB)
-    (1920, 1080, 64, (8, 8)),       # C5 (round 5: 8M runs, was 16 x 4 spp)
+    (1920, 1080, 64, (16, 4)),      # C5
     (256, 256, 64, (64, 1)),        # C1: capped at kMaxChunks
     (48, 32, 4, (4, 1)),
     (20, 12, 5, (3, 2)),            # 4 runs of 2 would leave one empty: trimmed to 3
-    (4000, 4000, 9, (1, 9)),        # 16M pixels: already past 8M runs, and 9 spp cannot make two 8-spp chunks
+    (4000, 4000, 9, (2, 5)),        # 16M pixels: two runs reach 32M work units
     (7, 3, 1, (1, 1)),
 ])
 def test_sample_chunk_rule(rt, w, h, spp, want):
