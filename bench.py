@@ -112,6 +112,13 @@ PMC_PASSES = (
 )
 
 
+# Each PMC child may take up to PMC_CHILD_TIMEOUT_S.  Under torchrun the other ranks wait
+# in init_process_group while rank 0 runs them, so the process group's rendezvous
+# timeout must outlast all of them (torch's default is 10 min for nccl): DIST_TIMEOUT_S.
+PMC_CHILD_TIMEOUT_S = 900
+DIST_TIMEOUT_S = len(PMC_PASSES) * PMC_CHILD_TIMEOUT_S + 600
+
+
 def kernel_instance(tuning):
     """The timed path-kernel instance's template arguments from the scene's resolved
     form (rt_scene_get_tuning; render.hip path_fn_r): <ST, HIT, WAVES, RES, KM, CMP>."""
@@ -211,7 +218,7 @@ def pmc_counters(args, world):
                    "--warmup", "0", "--no-cpu-baseline", "--no-pmc", "--as-rank0-of", str(world)]
             cmd += ["--tune", args.tune] if args.tune else []
             cmd += ["--spp", str(args.spp)] if args.spp else []
-            r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env)
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=PMC_CHILD_TIMEOUT_S, env=env)
             if r.returncode != 0:
                 return None, f"rocprofv3 --pmc {' '.join(counters)} failed rc={r.returncode}: {r.stderr[-300:]}"
             rows = []
@@ -398,10 +405,15 @@ def cpu_baseline(desc, params, target_s, runs=3):
                            "oracle_build_s": build_s,
                            "flags": "-O3 -march=native" if variant == "native" else "-O3 (portable)"}
         del osc
-    ok = max((v for v in ("native", "portable") if "median" in builds.get(v, {})), key=lambda v: builds[v]["median"])
+    done = [v for v in ("native", "portable") if "median" in builds.get(v, {})]
+    out["builds"] = builds
+    if not done:  # no oracle build on this host: report the errors, keep the GPU line
+        out["value"] = None
+        out["value_build"] = None
+        return out
+    ok = max(done, key=lambda v: builds[v]["median"])
     out["value"] = builds[ok]["median"]
     out["value_build"] = ok
-    out["builds"] = builds
     out["sample"] = (f"rows {rows[0]}..{rows[1]} of {params.width}x{params.height} at {params.spp} spp "
                      f"({paths} paths, {segs} segments per run), recursive raytrace_impl, OpenMP dynamic over "
                      f"pixels; median of {runs} runs per build")
@@ -452,10 +464,12 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
+        import datetime
+        pg_timeout = datetime.timedelta(seconds=DIST_TIMEOUT_S)  # rank 0's PMC passes come first
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=pg_timeout)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=pg_timeout)
     rt = load_package()
 
     scene_file, W, H, spp, depth = WORKLOADS[args.workload]
@@ -657,7 +671,8 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(desc, params, args.cpu_seconds)
-            out["speedup_vs_cpu"] = value / out["cpu_baseline"]["value"]
+            cb = out["cpu_baseline"]["value"]
+            out["speedup_vs_cpu"] = value / cb if cb else None
         # the PPM payload of the last frame (outside the timed region): identical for any N
         out["image_sha256"] = hashlib.sha256(image.cpu().numpy().tobytes()).hexdigest()
         print(json.dumps(out), flush=True)

@@ -110,6 +110,7 @@ class rt_tuning(C.Structure):
 
 TUNING_AUTO = dict(waves=0, resume=-1, kinds=0, suspend_lanes=0, leaf_lanes=0, chunk_spp=0, compact=-1, tail_split=0)
 RT_LAYOUT_COMPACT_TRIS = 0x1
+RT_LAYOUT_PAIR_NODES = 0x4
 
 
 # every symbol include/rt_api.h declares (checked by tests/test_abi.py)
@@ -117,6 +118,7 @@ EXPORTS = {
     "rt_scene_create": (C.c_int, [C.POINTER(rt_scene_desc), C.POINTER(C.c_void_p)]),
     "rt_scene_destroy": (None, [C.c_void_p]),
     "rt_scene_get_info": (C.c_int, [C.c_void_p, C.POINTER(rt_scene_info)]),
+    "rt_scene_checksum": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
     "rt_scene_set_tuning": (C.c_int, [C.c_void_p, C.POINTER(rt_tuning)]),
     "rt_scene_get_tuning": (C.c_int, [C.c_void_p, C.POINTER(rt_tuning)]),
     "rt_scene_sample_chunks": (C.c_int, [C.c_void_p, C.POINTER(rt_render_params), C.POINTER(C.c_uint32),
@@ -370,6 +372,12 @@ class Scene:
     def handle(self):
         return self._h
 
+    def checksum(self) -> int:
+        """rt_scene_checksum: content hash of the scene's device arrays."""
+        h = C.c_uint64()
+        _check(lib().rt_scene_checksum(self._h, C.byref(h)))
+        return h.value
+
     def info(self) -> dict:
         i = rt_scene_info()
         _check(lib().rt_scene_get_info(self._h, C.byref(i)))
@@ -500,6 +508,16 @@ class MultiScene:
             self.close()
         except Exception:
             pass
+
+    def scene_checksum(self, index: int) -> int:
+        """rt_scene_checksum of the replica on devices[index] (rt_multi_create already
+        checked every replica against devices[0]'s)."""
+        h = lib().rt_multi_scene(self._h, index)
+        if not h:
+            raise IndexError(index)
+        v = C.c_uint64()
+        _check(lib().rt_scene_checksum(C.c_void_p(h), C.byref(v)))
+        return v.value
 
     def scene_info(self, index: int) -> dict:
         """rt_scene_get_info of the replica on devices[index] (rt_multi_scene): devices[0]'s came

@@ -71,8 +71,10 @@ struct rt_scene {
     hipEvent_t ws_done = nullptr;
     // bytes of the triangle BVH's compact layout (nodes + leaf blocks), 0 without one
     uint64_t compact_bytes = 0;
+    uint64_t pair_bytes = 0;  // the pair layout's lines + the compact leaf blocks, 0 without one
     // requested kernel form (rt_scene_set_tuning); auto fields resolve per scene
     rt_tuning tune{0, -1, 0, 0, 0, 0, -1, 0};
+    uint32_t last_tail_split = 0;  // the split the last prepared frame resolved to (0: none since set_tuning)
 };
 
 namespace {
@@ -114,6 +116,7 @@ int upload_bvh(rt_scene* s, const HostBvhArrays& h, DevBvh& d) {
     if ((rc = upload(s, h.gid, &d.gid))) return rc;
     if ((rc = upload(s, h.cnodes, &d.cnodes))) return rc;
     if ((rc = upload(s, h.ctris, &d.ctris))) return rc;
+    if ((rc = upload(s, h.pnodes, &d.pnodes))) return rc;
     return RT_OK;
 }
 
@@ -327,6 +330,9 @@ int path_kinds(const rt_scene* s) { return s->tune.kinds == 3 ? 3 : scene_kinds(
 bool path_compact(const rt_scene* s) {
     return s->tune.compact != 0 && s->dev.tris.cnodes && path_waves(s) == 4 && path_resume(s) && path_kinds(s) == 2;
 }
+// The pair layout over the compact nodes (rt_layout.h kPairFloats, render.hip trav_step
+// PAIR: two BVH levels per dependent line): rt_tuning.compact = 2.
+bool path_pairs(const rt_scene* s) { return s->tune.compact == 2 && s->dev.tris.pnodes && path_compact(s); }
 
 
 
@@ -337,6 +343,7 @@ bool path_compact(const rt_scene* s) {
 // layout the kernel reads (path_compact: 64-B nodes and 36-B records, else 128 B
 // and 80 B).
 uint64_t bvh_hot_bytes(const rt_scene* s) {
+    if (path_pairs(s)) return s->pair_bytes;
     if (path_compact(s)) return s->compact_bytes;
     return s->info.bvh_nodes[2] * sizeof(DevNode) + s->info.n_triangles * sizeof(DevTri);
 }
@@ -364,7 +371,7 @@ int prepare_path(rt_scene* s, KParams& k, bool stats, bool hits, PathWork& W) {
     std::memset(&W, 0, sizeof(W));
     W.waves = path_waves(s);
     W.resume = path_resume(s);
-    W.kinds = path_compact(s) ? kKindsCompact : path_kinds(s);
+    W.kinds = path_pairs(s) ? kKindsPair : (path_compact(s) ? kKindsCompact : path_kinds(s));
     HIP_TRY(path_grid(stats, hits, W.waves, W.resume, W.kinds, (uint32_t)n_units, &W.grid));
     const uint64_t lanes = (uint64_t)W.grid * 64u;
     int rc;
@@ -401,6 +408,7 @@ int prepare_path(rt_scene* s, KParams& k, bool stats, bool hits, PathWork& W) {
     }
     k.n_tail = (uint32_t)tail;
     k.tail_split = tail ? split : 1u;
+    s->last_tail_split = k.tail_split;  // rt_scene_get_tuning reports what the frame resolved to
     k.rows = s->rows;
     W.queue = s->queue; W.ring = s->ring; W.part = s->part;
     W.d_scene = s->d_scene; W.d_params = s->d_params;
@@ -410,8 +418,13 @@ int prepare_path(rt_scene* s, KParams& k, bool stats, bool hits, PathWork& W) {
 
 // device counters (render.hip wave_flush order) -> rt_stats (timings untouched)
 int copy_stats(rt_scene* s, rt_stats* out) {
-    unsigned long long c[kNStats];
+    unsigned long long c[kStatStall + 1];
     HIP_TRY(hipMemcpy(c, s->d_stats, sizeof(c), hipMemcpyDeviceToHost));
+    // the stats instance's progress guard (render.h kStatStall): a wave that looped
+    // without progress exited early, so the frame is incomplete — fail loudly
+    if (c[kStatStall])
+        return set_error(RT_ERR_DEVICE, "path kernel: " + std::to_string(c[kStatStall]) + " wave(s) made no progress "
+                                        "for " + std::to_string(kStallTrips) + " loop trips (livelock guard)");
     out->paths = c[0]; out->segments = c[1]; out->aabb_tests = c[2]; out->tri_tests = c[3];
     out->shape_tests = c[4]; out->shaded_hits = c[5]; out->light_queries = c[6]; out->light_hits = c[7];
     out->lane_steps = c[8]; out->wave_steps = c[9];
@@ -614,7 +627,9 @@ int scene_upload(const HostScene& hs, rt_scene** out, bool replica) {
     s->info.n_light_triangles = d.ltris.n_prims;
     s->info.shared_light_mask = d.slt_mask;
     s->compact_bytes = hs.bvh[2].cnodes.size() * sizeof(DevNodeC) + hs.bvh[2].ctris.size() * sizeof(float);
-    s->info.layout_flags = (d.tris.cnodes ? RT_LAYOUT_COMPACT_TRIS : 0u) | (d.lq_boxes ? RT_LAYOUT_LQ_SKIP : 0u);
+    s->pair_bytes = (hs.bvh[2].pnodes.size() + hs.bvh[2].ctris.size()) * sizeof(float);
+    s->info.layout_flags = (d.tris.cnodes ? RT_LAYOUT_COMPACT_TRIS : 0u) | (d.lq_boxes ? RT_LAYOUT_LQ_SKIP : 0u) |
+                           (d.tris.pnodes ? RT_LAYOUT_PAIR_NODES : 0u);
     s->info.build_ms = hs.build_ms;
     s->info.upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     *out = owner.release();
@@ -665,7 +680,7 @@ int rt_scene_sample_chunks(const rt_scene* s, const rt_render_params* p, uint32_
 
 int rt_scene_set_tuning(rt_scene* s, const rt_tuning* t) {
     if (!s) return set_error(RT_ERR_INVALID, "scene is NULL");
-    if (!t) { s->tune = rt_tuning{0, -1, 0, 0, 0, 0, -1, 0}; return RT_OK; }
+    if (!t) { s->tune = rt_tuning{0, -1, 0, 0, 0, 0, -1, 0}; s->last_tail_split = 0; return RT_OK; }
     if (t->waves != 0 && (t->waves < 3 || t->waves > 5)) return set_error(RT_ERR_INVALID, "waves must be 0, 3, 4 or 5");
     if (t->resume < -1 || t->resume > 1) return set_error(RT_ERR_INVALID, "resume must be -1, 0 or 1");
     if (t->kinds > 3) return set_error(RT_ERR_INVALID, "kinds must be 0..3");
@@ -673,11 +688,30 @@ int rt_scene_set_tuning(rt_scene* s, const rt_tuning* t) {
     if ((t->kinds == 1 || t->kinds == 2) && (int)t->kinds != scene_kinds(s->dev))
         return set_error(RT_ERR_INVALID, "kinds 1/2 must be the scene's own primitive kinds (0 or 3 otherwise)");
     if (t->suspend_lanes > 64 || t->leaf_lanes > 64) return set_error(RT_ERR_INVALID, "lane counts must be <= 64");
-    if (t->compact < -1 || t->compact > 1) return set_error(RT_ERR_INVALID, "compact must be -1, 0 or 1");
-    if (t->compact == 1 && !s->dev.tris.cnodes)
-        return set_error(RT_ERR_UNSUPPORTED, "compact = 1: the scene has no compact triangle layout");
+    if (t->compact < -1 || t->compact > 2) return set_error(RT_ERR_INVALID, "compact must be -1, 0, 1 or 2");
+    if (t->compact >= 1 && !s->dev.tris.cnodes)
+        return set_error(RT_ERR_UNSUPPORTED, "compact >= 1: the scene has no compact triangle layout");
+    if (t->compact == 2 && !s->dev.tris.pnodes)
+        return set_error(RT_ERR_UNSUPPORTED, "compact = 2: the scene has no pair layout");
     if (t->tail_split > 8) return set_error(RT_ERR_INVALID, "tail_split must be 0..8");
     s->tune = *t;
+    s->last_tail_split = 0;
+    return RT_OK;
+}
+
+int rt_scene_checksum(rt_scene* s, uint64_t* out) {
+    if (!s || !out) return set_error(RT_ERR_INVALID, "scene/out is NULL");
+    DEVICE_GUARD(s);
+    const size_t n = s->allocs.size();
+    DevBuf<unsigned long long> sums;
+    HIP_TRY(sums.alloc(std::max<size_t>(n, 1)));
+    for (size_t k = 0; k < n; ++k) HIP_TRY(launch_checksum(s->allocs[k], s->alloc_bytes[k], sums.p + k, 0));
+    std::vector<unsigned long long> h(n);
+    HIP_TRY(hipDeviceSynchronize());
+    if (n) HIP_TRY(hipMemcpy(h.data(), sums.p, n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    uint64_t acc = 0xcbf29ce484222325ull;  // arrays in allocation order, each with its size
+    for (size_t k = 0; k < n; ++k) acc = (acc ^ (h[k] + 0x9e3779b97f4a7c15ull * s->alloc_bytes[k])) * 0x100000001b3ull;
+    *out = acc;
     return RT_OK;
 }
 
@@ -689,8 +723,8 @@ int rt_scene_get_tuning(const rt_scene* s, rt_tuning* out) {
     out->suspend_lanes = path_suspend(s);
     out->leaf_lanes = path_leaf_batch(s);
     out->chunk_spp = s->tune.chunk_spp;
-    out->compact = path_compact(s) ? 1 : 0;
-    out->tail_split = s->tune.tail_split ? s->tune.tail_split : kTailSplit;
+    out->compact = path_pairs(s) ? 2 : (path_compact(s) ? 1 : 0);
+    out->tail_split = s->last_tail_split ? s->last_tail_split : (s->tune.tail_split ? s->tune.tail_split : kTailSplit);
     return RT_OK;
 }
 

@@ -220,6 +220,18 @@ int replicate_scene(rt_multi* m) {
     }
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     for (uint32_t i = 1; i < n; ++i) rt::scene_add_upload_ms(m->scenes[i], ms);
+    // every replica must hold devices[0]'s bytes (a wrong root, buffer pairing or array
+    // order would otherwise render silently wrong frames): content hashes on each device
+    uint64_t h0 = 0;
+    if (int rc = rt_scene_checksum(m->scenes[0], &h0)) return rc;
+    for (uint32_t i = 1; i < n; ++i) {
+        uint64_t h = 0;
+        if (int rc = rt_scene_checksum(m->scenes[i], &h)) return rc;
+        if (h != h0)
+            return set_error(RT_ERR_DEVICE, "scene replica on device " + std::to_string(m->devs[i]) +
+                                                " differs from devices[0]'s after the " +
+                                                (m->peer ? "peer copies" : "ncclBroadcast"));
+    }
     return RT_OK;
 }
 

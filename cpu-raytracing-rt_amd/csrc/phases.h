@@ -16,11 +16,14 @@ namespace rt {
 // stack pops, kPhStepCyc whole steps (kPhTris minus it: the loop around them).
 // Regions timed with PH_ADDW also add cycles x (active lanes / 64) at k + kPhW:
 // the ratio of the two is the region's lane utilisation.  kPhInnerUni counts the
-// compact inner-node wave steps whose lanes all visit the same node.
+// compact inner-node wave steps whose lanes all visit the same node.  kPhIdleWin /
+// kPhIdleDrain count, per path-loop trip, the lanes left without a path after the
+// hand-out: held by the commit window (or the open wave-tile cap) while the queue
+// still has work, vs the queue drained (the launch tail).
 enum { kPhAssign, kPhIntersect, kPhLightSample, kPhLightPdf, kPhSegment, kPhCommit, kPhTile,
        kPhTravWave, kPhTravLane, kPhLeafWave, kPhLeafLane, kPhRngWave, kPhRngLane, kPhW0,
        kPhPlanes = kPhW0 + 5, kPhBoxes, kPhElls, kPhTris, kPhMaterialise,
-       kPhInnerWave, kPhInnerLane, kPhLiveLane, kPhRngFallWave, kPhRngFallLane,
+       kPhInnerWave, kPhInnerLane, kPhLiveLane, kPhIdleWin, kPhIdleDrain,
        kPhPushLane, kPhPushGlobal, kPhPopGlobal, kPhLeafCyc, kPhInnerCyc, kPhPopCyc, kPhStepCyc, kPhInnerUni, kPhN };  // traversal-stack pushes, past the LDS part
 static_assert(16 + kPhN <= 52, "phase words fit the raw stats below the timeline words (render.h kTimeline)");
 constexpr int kPhW = kPhW0 - kPhIntersect;  // weighted word of region k = k + kPhW (k in 1..5)

@@ -42,6 +42,14 @@ constexpr int kStatLqSkip = 10;  // raw word: last-bounce light queries the time
 // raw words 11..13: inner-node visits of closest-hit traversals whose child boxes
 // were hit by none / one / both of the two slab tests (stats instances only)
 constexpr int kStatKids0 = 11;
+// raw word 14 (stats path kernel only): waves that made no progress for kStallTrips
+// consecutive loop trips and exited (render.hip path_kernel's progress guard; the
+// host turns a nonzero word into RT_ERR_DEVICE, api.cpp copy_stats).  A trip makes
+// progress when it pulls a wave-tile, hands out a path, steps a traversal, shades a
+// segment or commits a row; a wave with nothing of that left has exited, so an idle
+// trip can only be a livelock (the round-5 RT_RING_ROWS=16 build's).
+constexpr int kStatStall = 14;
+constexpr uint32_t kStallTrips = 256;
 constexpr int kTimeline = 52;     // stats path kernel: wave timeline words 52..59 (render.hip, tools/timeline.py)
 constexpr int kPhaseWord0 = 16;   // RT_PHASES builds: region cycles + loop counts at words 16..51 (16 + kPhN - 1)
 
@@ -78,6 +86,9 @@ inline void sample_chunks(uint32_t W, uint32_t H, uint32_t spp, uint32_t& chunks
 // compact layout (rt_layout.h DevNodeC): kTris | 4, only with the 4-wave
 // resumable instance (api.cpp path_kinds).
 constexpr int kKindsCompact = 6;
+// ... with its inner nodes read from the pair layout (rt_layout.h kPairFloats):
+// kTris | 4 | 8, the same instance family (api.cpp path_pairs).
+constexpr int kKindsPair = 14;
 
 // Device workspace of one path-kernel launch (owned by the scene).
 struct PathWork {
@@ -158,6 +169,8 @@ hipError_t launch_unpack(const double* g, double* img, uint32_t W, uint32_t H, u
                          uint32_t per_rank, hipStream_t st);
 // ellipsoid records: aux = dev_rcp(radii), the device's own reciprocals (rt_device.h)
 hipError_t launch_ell_rcp(DevShape* shapes, uint32_t n, hipStream_t st);
+// checksum_kernel: order-free content hash of a device array (rt_scene_checksum)
+hipError_t launch_checksum(const void* p, uint64_t bytes, unsigned long long* d_out, hipStream_t st);
 hipError_t launch_fp64_probe(const double* a, const double* b, double* out, uint32_t n, int op, hipStream_t st);
 
 }  // namespace rt

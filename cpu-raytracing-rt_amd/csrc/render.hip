@@ -282,7 +282,9 @@ RT_D TriRec load_tri_c(const float* __restrict__ p) {
 // CMP: the triangle BVH's compact layout (DevBvh::cnodes / ctris, KIND 3 only):
 // the same boxes and vertices as exact f32 copies, widened to f64 before the
 // same arithmetic — every lane's visits, tests and results are the f64 form's.
-template <int KIND, int SLAB, bool ST, bool CMP = false, class Stk>
+// PAIR (with CMP): inner nodes from the pair layout (rt_layout.h kPairFloats), two BVH
+// levels per line — see the branch below.
+template <int KIND, int SLAB, bool ST, bool CMP = false, bool PAIR = false, class Stk>
 RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk& S, Cnt<ST>& C, Trav& T,
                     uint64_t lv, int leaf_batch = kLeafBatch) {
     const unsigned long long ph_st = PH_T();
@@ -355,6 +357,77 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
             next = true;
         }
         PH_ADD(kPhLeafCyc, ph_l);
+    } else if (PAIR && T.live && T.cnt == 0) {  // internal node, pair layout: up to two visits
+        // Visit c = T.node: its line holds, per child K, the boxes a visit of K tests (K
+        // internal; K's own box is their union — exact, build_pairs) or K's box (a leaf).
+        // Both children are tested as in the compact branch (bvh.rs:158-185), then, when
+        // the near child K is internal, K is visited at once from the same line — what the
+        // reference does next (K has no primitives; `best` is unchanged) — so one dependent
+        // load serves two levels.  Every visit counts as in the compact form (C.aabb / kids).
+        const unsigned long long ph_i = PH_T();
+        const float4* nw = (const float4*)(B.pnodes + (size_t)T.node * kPairFloats);
+        const float4 a0 = nw[0], a1 = nw[1], a2 = nw[2];
+        const uint4 aw = ((const uint4*)nw)[3];
+        const float4 b0 = nw[4], b1 = nw[5], b2 = nw[6];
+        const uint4 bw = ((const uint4*)nw)[7];
+        asm volatile("" ::"v"(b0.x), "v"(b0.y), "v"(b0.z), "v"(b0.w), "v"(b1.x), "v"(b1.y), "v"(b1.z), "v"(b1.w),
+                     "v"(b2.x), "v"(b2.y), "v"(b2.z), "v"(b2.w), "v"(bw.z), "v"(bw.w));  // one batch: see node_boxes
+        PH_COUNT(kPhInnerWave, kPhInnerLane);
+        // half: A = (x0.xyz | x0.w x1.xy), B = (x1.zw x2.x | x2.yzw); a leaf child's box is A
+        const bool la = aw.w & kPairLeaf, lb = bw.w & kPairLeaf;
+        const float lmnx = la ? a0.x : fminf(a0.x, a1.z), lmny = la ? a0.y : fminf(a0.y, a1.w),
+                    lmnz = la ? a0.z : fminf(a0.z, a2.x), lmxx = la ? a0.w : fmaxf(a0.w, a2.y),
+                    lmxy = la ? a1.x : fmaxf(a1.x, a2.z), lmxz = la ? a1.y : fmaxf(a1.y, a2.w);
+        const float rmnx = lb ? b0.x : fminf(b0.x, b1.z), rmny = lb ? b0.y : fminf(b0.y, b1.w),
+                    rmnz = lb ? b0.z : fminf(b0.z, b2.x), rmxx = lb ? b0.w : fmaxf(b0.w, b2.y),
+                    rmxy = lb ? b1.x : fmaxf(b1.x, b2.z), rmxz = lb ? b1.y : fmaxf(b1.y, b2.w);
+        C.aabb(2);
+        double lt = 0.0, rt2 = 0.0;
+        const bool lh = slab_c<SLAB>(lmnx, lmny, lmnz, lmxx, lmxy, lmxz, o, d, rc, fast, lt);
+        const bool rh = slab_c<SLAB>(rmnx, rmny, rmnz, rmxx, rmxy, rmxz, o, d, rc, fast, rt2);
+        C.kids(lh, rh);
+        double bt = T.best;  // +inf when no hit yet
+        double li = lh ? (lt < bt ? lt : bt) : bt;
+        double ri = rh ? (rt2 < bt ? rt2 : bt) : bt;
+        bool go_left = false, push = false;
+        uint32_t pw = 0;
+        double pt = 0.0;
+        if (li < bt) {
+            if (ri < bt) {
+                push = true;
+                if (li < ri) { pw = bw.z; pt = ri; go_left = true; }
+                else { pw = aw.z; pt = li; }
+            } else go_left = true;
+        } else if (!(ri < bt)) next = true;
+        if (push) S.push(pw, pt);
+        if (!next) {
+            // the near child K: a leaf is entered by its word; an internal one is visited now
+            const bool kl = go_left ? la : lb;
+            if (kl) {
+                trav_enter<true>(B, T, go_left ? aw.z : bw.z);
+            } else {
+                const float4 k0 = go_left ? a0 : b0, k1 = go_left ? a1 : b1, k2 = go_left ? a2 : b2;
+                const uint32_t kx = go_left ? aw.x : bw.x, ky = go_left ? aw.y : bw.y;
+                C.aabb(2);
+                const bool lh2 = slab_c<SLAB>(k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, o, d, rc, fast, lt);
+                const bool rh2 = slab_c<SLAB>(k1.z, k1.w, k2.x, k2.y, k2.z, k2.w, o, d, rc, fast, rt2);
+                C.kids(lh2, rh2);
+                li = lh2 ? (lt < bt ? lt : bt) : bt;
+                ri = rh2 ? (rt2 < bt ? rt2 : bt) : bt;
+                go_left = false;
+                push = false;
+                if (li < bt) {
+                    if (ri < bt) {
+                        push = true;
+                        if (li < ri) { pw = ky; pt = ri; go_left = true; }
+                        else { pw = kx; pt = li; }
+                    } else go_left = true;
+                } else if (!(ri < bt)) next = true;
+                if (push) S.push(pw, pt);
+                if (!next) trav_enter<true>(B, T, go_left ? kx : ky);
+            }
+        }
+        PH_ADD(kPhInnerCyc, ph_i);
     } else if (CMP && T.live && T.cnt == 0) {  // internal node, compact layout (64 B)
         // both children's f32 boxes and their two child words (56 of the 64 B: a leaf's
         // own range is read by trav_enter)
@@ -1470,7 +1543,7 @@ RT_D uint32_t unit_of_row(const uint32_t* uq, uint32_t uq_back, uint32_t row) {
 }
 
 
-template <bool ST, bool HIT, int WAVES, bool RES, int KM = 3, bool CMP = false>
+template <bool ST, bool HIT, int WAVES, bool RES, int KM = 3, bool CMP = false, bool PAIR = false>
 __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams Pv,
                                                      const DevScene* __restrict__ Sg,
                                                      const KParams* __restrict__ Pg, double* __restrict__ out,
@@ -1535,6 +1608,7 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
     SegQuery q;
     q.T.live = false;
     bool inq = false;  // this lane's segment query is under way
+    uint32_t stall = 0;  // stats instance: consecutive trips without progress (kStatStall)
     for (;;) {
         // fields s_load'ed where used (see opaque), for both register budgets
         // (C3 at 64 spp: 315.6 vs 325.9 ms with the by-value kernel
@@ -1545,6 +1619,8 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
         const Scales sc{P.scale01, P.scale11};
         const uint64_t idle = __ballot(!busy);
         const unsigned long long ph_a = PH_T();
+        const uint32_t prog0 = next + base + uq_back + (drained ? 1u : 0u);  // ST: the progress guard
+        bool worked = false;  // ST: a traversal step or a shaded segment in this trip
         // pull wave-tiles until the rows the idle lanes could take exist (inside the
         // commit window of kRing rows, at most kUQ open)
         const uint32_t window = (base + kRing) * kWave;
@@ -1633,6 +1709,12 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
             next = min(limit, next + (uint32_t)__popcll(idle));
         }
         PH_ADD(kPhAssign, ph_a);
+#ifdef RT_PHASES
+        if (!busy) {  // why this lane has no path this trip
+            if (drained && next >= open_end * kWave) PH_LANE(kPhIdleDrain);
+            else PH_LANE(kPhIdleWin);
+        }
+#endif
         bool ends = false;  // this lane's path ends in this trip
         if constexpr (RES) {
             // lanes between segments (new paths, continued paths) start their query
@@ -1656,12 +1738,14 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
                                           (!drained && next < win && uq_back - uq_front < kUQ);
                     if (__ballot((busy && !q.T.live) || (!busy && can_take))) break;
                 }
-                trav_step<3, 2, ST, CMP>(S.tris, ps.o, ps.d, q.rc, q.fast, stk, C, q.T, lv, (int)P.leaf_batch);
+                trav_step<3, 2, ST, CMP, PAIR>(S.tris, ps.o, ps.d, q.rc, q.fast, stk, C, q.T, lv, (int)P.leaf_batch);
+                if (ST) worked = true;
             }
             PH_ADD(kPhTris, ph_t);
             // lanes whose query finished shade and end (or continue) their segment
             if (busy && !q.T.live) {
                 C.step();
+                if (ST) worked = true;
                 bool cont = false;
                 if (inq) {
                     int32_t g;
@@ -1678,6 +1762,7 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
             }
         } else if (busy) {  // fused: one whole segment of every live path
             C.step();
+            if (ST) worked = true;
             bool cont = false;
             if (b < depth) {
                 int32_t g;
@@ -1734,6 +1819,16 @@ __global__ __launch_bounds__(kWave, WAVES) void path_kernel(DevScene Sv, KParams
         }
         PH_ADD(kPhCommit, ph_c);
         if (drained && uq_front == uq_back) break;  // every pulled wave-tile written
+        if constexpr (ST) {
+            // Progress guard (render.h kStatStall): a trip that pulls, hands out, steps,
+            // shades or commits nothing can only repeat itself — flag the wave and exit.
+            const bool moved = __ballot(worked) != 0 || next + base + uq_back + (drained ? 1u : 0u) != prog0;
+            stall = moved ? 0u : stall + 1u;
+            if (stall >= kStallTrips) {
+                if (lane == 0) atomicAdd(&stats[kStatStall], 1ull);
+                break;
+            }
+        }
     }
     wave_flush<ST>(C, stats, witers);
     if (ST && lane == 0) {
@@ -1920,10 +2015,12 @@ PathFn path_fn_r(uint32_t waves, bool resume, int kinds) {
 #else
     if (kinds == kKindsCompact) return path_kernel<ST, HIT, 4, true, kTris, true>;
 #endif
+    if (kinds == kKindsPair) return path_kernel<ST, HIT, 4, true, kTris, true, true>;
     return kinds == kTris ? path_kernel<ST, HIT, 4, true, kTris> : path_kernel<ST, HIT, 4, true>;
 #else
     if (waves == 4 && resume) {
         if (kinds == kKindsCompact) return path_kernel<ST, HIT, 4, true, kTris, true>;  // compact triangle layout
+        if (kinds == kKindsPair) return path_kernel<ST, HIT, 4, true, kTris, true, true>;  // + pair layout
         return kinds == kTris ? path_kernel<ST, HIT, 4, true, kTris> : path_kernel<ST, HIT, 4, true>;
     }
     kinds &= 3;  // the compact layout has only the triangle-only resumable instance (host: path_kinds)
@@ -1962,6 +2059,10 @@ hipError_t launch_path(const DevScene& S, const KParams& P, const PathWork& W, d
     if (W.waves < 3 || W.waves > 5 || (W.waves == 5 && (W.resume || W.kinds != kShapes))) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(W.queue, 0, kQueueWords * sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
+    // the stats instance's wave timeline (words kTimeline..+7) describes ONE launch: it
+    // is cleared here, while the counters accumulate until rt_read_stats resets them
+    if (stats && (e = hipMemsetAsync(stats + kTimeline, 0, 8 * sizeof(unsigned long long), st)) != hipSuccess)
+        return e;
     // the frame constants travel by pointer (see opaque): stage them in the scene's
     // slot, stream-ordered (the by-value argument is captured at launch)
     hipLaunchKernelGGL(stage_params_kernel, dim3(1), dim3(1), 0, st, W.d_params, P);
@@ -1978,6 +2079,38 @@ hipError_t launch_path(const DevScene& S, const KParams& P, const PathWork& W, d
     }
     if (e != hipSuccess || P.chunks == 1) return e;
     return launch_reduce_chunks(W.part, out, P, st);
+}
+
+// Content checksum of a device array (rt_scene_checksum; multi.cpp checks every
+// replica against devices[0]'s after the fill): word i (8 B, little-endian, the last
+// one zero-padded) contributes splitmix64(w + i * golden) to a 64-bit sum — order-free,
+// so the atomics keep it deterministic, and a word moved, changed or missing shows.
+RT_D uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+__global__ void checksum_kernel(const uint8_t* __restrict__ p, uint64_t bytes, unsigned long long* __restrict__ out) {
+    const uint64_t words = (bytes + 7) / 8, full = bytes / 8;
+    const uint64_t* w = (const uint64_t*)p;
+    uint64_t h = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t v = 0;
+        if (i < full) v = w[i];
+        else for (uint64_t b = 8 * i; b < bytes; ++b) v |= (uint64_t)p[b] << (8 * (b - 8 * i));
+        h += mix64(v + i * 0x9e3779b97f4a7c15ull);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) h += __shfl_xor(h, off, 64);
+    if ((threadIdx.x & 63) == 0 && h) atomicAdd(out, (unsigned long long)h);
+}
+hipError_t launch_checksum(const void* p, uint64_t bytes, unsigned long long* d_out, hipStream_t st) {
+    hipError_t e = hipMemsetAsync(d_out, 0, sizeof(*d_out), st);
+    if (e != hipSuccess || bytes == 0) return e;
+    const uint64_t words = (bytes + 7) / 8;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(2048, (words + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(checksum_kernel, dim3(blocks), dim3(kBlock), 0, st, (const uint8_t*)p, bytes, d_out);
+    return hipGetLastError();
 }
 
 // The queue's tail wave-tiles (queue_entry): each pixel's rows summed in sample order

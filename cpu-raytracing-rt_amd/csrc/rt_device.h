@@ -99,7 +99,6 @@ RT_D void rng_init(Rng& r, uint64_t seed, uint64_t pixel, uint32_t sample) {
 // Fallback for the rare draw that finds no next block ready.
 RT_D void philox_next(Rng& r) {
     PH_COUNT(kPhRngWave, kPhRngLane);
-    PH_COUNT(kPhRngFallWave, kPhRngFallLane);
     philox(r.blk, r.sample, r.pix_lo, r.pix_hi, r.k0, r.k1, r.n0, r.n1);
     r.blk++;
     r.nready = 1;

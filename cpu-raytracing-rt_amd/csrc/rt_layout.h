@@ -78,6 +78,17 @@ constexpr uint32_t kTriC = 9;   // floats per compact triangle record
 // 128-B line; a leaf's child word / big-leaf entry carries the block index.
 constexpr uint32_t kLeafBlock = 32;  // floats per 128-B line
 
+// Pair layout (round 6, scene_build.cpp build_pairs): one 128-B line per internal
+// compact slot c, two 64-B halves for c's left and right child K:
+//   floats 0..5  box A, 6..11 box B, then words 12 A's word, 13 B's word, 14 K's own
+//   word (its child word in c), 15 flags.
+// K internal: A / B = K's children's boxes and words (what a visit of K tests); K's own
+// box is their union.  K a leaf (flags kPairLeaf): A = K's box.  A visit of c reads
+// c's line, tests both children and can visit the near child K from the same line:
+// two BVH levels per dependent load.  Slot indices are the compact ones.
+constexpr uint32_t kPairFloats = 32, kPairHalf = 16;
+constexpr uint32_t kPairLeaf = 1u;
+
 struct alignas(16) DevShape {  // Primitive<T> hot part (scene.rs:20-27)
     double shape[3];           // plane normal | box half sizes | ellipsoid radii
     double pos[3];
@@ -138,6 +149,7 @@ struct DevBvh {
     // non-null only when every box coordinate and vertex is an exact f32
     const DevNodeC* cnodes;
     const float* ctris;
+    const float* pnodes;       // pair layout (kPairFloats per internal compact slot) or null
 };
 
 struct DevScene {

@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cmath>
 #include <cstring>
 #include <thread>
 
@@ -312,6 +313,44 @@ bool f32_exact3(V3 v) { return f32_exact(v.x) && f32_exact(v.y) && f32_exact(v.z
 // is an exact f32 (glTF positions are f32: C3-C5; a custom TRIANGLE rotated by a
 // quaternion usually is not).  The device widens them back to f64 and rebuilds
 // ba = b - a, ca = c - a: the bits triangle_props computed from the same a, b, c.
+// Pair layout of the compact triangle BVH (rt_layout.h kPairFloats, DESIGN.md §4 "two
+// levels per line"): record c (one 128-B line per internal slot c) holds, for each child
+// K of c, K's children's boxes and words when K is internal — the boxes a visit of K
+// tests — or K's own box when it is a leaf.  A visit of c then takes K's box as the union
+// of K's children's boxes (exact: a node's box is the union of its primitives' boxes,
+// bvh.rs:56-62, so the f32 min/max of the two children's boxes is the same box) and can
+// go on to visit the near child K from the same line.  Built only when that union
+// reproduces every internal child's box; otherwise left empty (the compact form stays).
+void build_pairs(HostBvhArrays& out, size_t n_int) {
+    const std::vector<DevNodeC>& cn = out.cnodes;
+    std::vector<float> pr(n_int * kPairFloats, 0.0f);
+    for (size_t c = 0; c < n_int; ++c) {
+        for (int side = 0; side < 2; ++side) {
+            float* h = &pr[c * kPairFloats + side * kPairHalf];
+            const uint32_t w = side ? cn[c].rw : cn[c].lw;
+            const float* mn = side ? cn[c].rmin : cn[c].lmin;
+            const float* mx = side ? cn[c].rmax : cn[c].lmax;
+            uint32_t words[4] = {0u, 0u, w, 0u};
+            if (w & (kPackedLeaf | kLeafRef)) {  // a leaf child: its own box
+                std::memcpy(h, mn, 3 * sizeof(float));
+                std::memcpy(h + 3, mx, 3 * sizeof(float));
+                words[3] = kPairLeaf;
+            } else {  // an internal child K = slot w: the boxes its visit tests, its words
+                const DevNodeC& k = cn[w];
+                std::memcpy(h, k.lmin, 3 * sizeof(float)); std::memcpy(h + 3, k.lmax, 3 * sizeof(float));
+                std::memcpy(h + 6, k.rmin, 3 * sizeof(float)); std::memcpy(h + 9, k.rmax, 3 * sizeof(float));
+                for (int a = 0; a < 3; ++a)
+                    if (std::fmin(k.lmin[a], k.rmin[a]) != mn[a] || std::fmax(k.lmax[a], k.rmax[a]) != mx[a])
+                        return;  // not the union: no pair layout for this BVH
+                words[0] = k.lw;
+                words[1] = k.rw;
+            }
+            std::memcpy(h + 12, words, sizeof(words));
+        }
+    }
+    out.pnodes = std::move(pr);
+}
+
 void build_compact(const HostBvh& h, const std::vector<TriItem>& items, HostBvhArrays& out) {
     for (const HostNode& n : h.nodes)
         if (!f32_exact3(n.box.min) || !f32_exact3(n.box.max)) return;
@@ -352,6 +391,7 @@ void build_compact(const HostBvh& h, const std::vector<TriItem>& items, HostBvhA
     for (size_t i = 0; i < h.nodes.size(); ++i)  // h.nodes is in pre-order
         if (h.nodes[i].left >= 0) slot[i] = (uint32_t)n_slots++;
     if (n_slots == 0 || slot[0] != 0) return;  // a leaf root: nothing to traverse
+    const size_t n_int = n_slots;
     for (size_t i = 0; i < h.nodes.size(); ++i)
         if (h.nodes[i].left < 0 && !packs(i)) slot[i] = (uint32_t)n_slots++;
     if (n_slots >= kLeafRef || n_floats / kLeafBlock >= (1ull << 32)) return;
@@ -398,6 +438,7 @@ void build_compact(const HostBvh& h, const std::vector<TriItem>& items, HostBvhA
     }
     out.cnodes = std::move(cn);
     out.ctris = std::move(ct);
+    build_pairs(out, n_int);
 }
 
 void build_tri_bvh(const std::vector<TriItem>& items, HostBvhArrays& out, bool compact = false) {

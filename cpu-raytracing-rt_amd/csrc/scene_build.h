@@ -54,6 +54,9 @@ struct HostBvhArrays {
     // triangle): filled only when every box coordinate and vertex is an exact f32
     std::vector<DevNodeC> cnodes;
     std::vector<float> ctris;
+    // pair layout over the compact nodes (rt_layout.h kPairFloats per internal slot),
+    // filled when every internal child's box is the union of its children's
+    std::vector<float> pnodes;
 };
 struct HostScene {
     std::vector<DevMaterial> mats;

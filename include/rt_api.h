@@ -177,7 +177,10 @@ typedef struct rt_scene_info {
     uint32_t bvh_depth[6];
     double   build_ms;           /* host BVH build                                */
     double   upload_ms;          /* H2D copy                                      */
-    uint64_t device_bytes;
+    uint64_t device_bytes;       /* the scene's arrays; the per-launch workspace (commit
+                                    ring, split-tail row buffer <= 256 MB, chunk partials
+                                    <= 4 GiB, stack spill) is grow-only, sized by the
+                                    largest frame rendered, and not counted here      */
     /* bit i: scene box i (BVH order) doubles as the next light box, so the light
        pdf of a diffuse bounce comes from the next segment's box tests (DESIGN.md
        §4 "shared light tests"); 0 = separate light queries */
@@ -192,7 +195,16 @@ typedef struct rt_scene_info {
 } rt_scene_info;
 #define RT_LAYOUT_COMPACT_TRIS 0x1u
 #define RT_LAYOUT_LQ_SKIP      0x2u
+/* RT_LAYOUT_PAIR_NODES: the compact triangle BVH also has its pair layout (one 128-B
+   line per inner node holding what a visit of either child tests, so a descent reads
+   one line per two levels), selected by rt_tuning.compact = 2 */
+#define RT_LAYOUT_PAIR_NODES   0x4u
 int rt_scene_get_info(const rt_scene* scene, rt_scene_info* out);
+/* Content hash of the scene's device arrays (BVHs, records, materials; not the
+   per-launch workspace), computed on the scene's device.  Two handles built from the
+   same description — or an rt_multi replica and devices[0]'s scene — hash equal;
+   rt_multi_create checks every replica this way after the fill. */
+int rt_scene_checksum(rt_scene* scene, uint64_t* out);
 
 /* Kernel form of a scene's renders.  The library picks every
    field from the scene itself ("auto"); a caller may force one for tests and
@@ -214,7 +226,8 @@ typedef struct rt_tuning {
                                 (rt_scene_sample_chunks reports the run length used)                    */
     int32_t  compact;        /* -1 auto (1 when the scene has it: RT_LAYOUT_COMPACT_TRIS); 0 the f64
                                 triangle-BVH layout; 1 the compact one (triangle-only resumable kernel;
-                                RT_ERR_UNSUPPORTED on a scene without RT_LAYOUT_COMPACT_TRIS)           */
+                                RT_ERR_UNSUPPORTED on a scene without RT_LAYOUT_COMPACT_TRIS); 2 the
+                                compact one with its pair layout (RT_LAYOUT_PAIR_NODES)               */
     uint32_t tail_split;     /* 0 auto (8); 1 every wave-tile whole; 2..8: the queue's last wave-tiles
                                 (three per resident wave) are handed out in this many parts of
                                 consecutive sample rows and summed in sample order after the launch
@@ -226,7 +239,9 @@ typedef struct rt_tuning {
 /* NULL restores every field to auto.  Fields out of range -> RT_ERR_INVALID. */
 int rt_scene_set_tuning(rt_scene* scene, const rt_tuning* tuning);
 /* The form the next render of this scene runs: auto fields resolved (chunk_spp
-   stays 0 when the frame's rule applies). */
+   stays 0 when the frame's rule applies).  tail_split: after a render, the split that
+   frame resolved to (1 when the split cannot apply: sample runs >= 65536 rows or no
+   room for a row buffer); before any render since rt_scene_set_tuning, the setting. */
 int rt_scene_get_tuning(const rt_scene* scene, rt_tuning* resolved);
 
 /* ======================= the frame (hot path) ============================= */
@@ -258,7 +273,13 @@ int rt_render_tiles_async(rt_scene* scene, const rt_render_params* params,
    count the inner-node visits of closest-hit BVH traversals whose two child boxes
    were hit by none / one / both slab tests; builds compiled
    with -DRT_PHASES add wave cycles and loop counts per path-kernel region at
-   words 16..51 (16 + kPhN - 1, phases.h; tools/phases.py).  Not needed to render. */
+   words 16..51 (16 + kPhN - 1, phases.h; tools/phases.py).  Word 14 counts waves
+   the stats kernel's progress guard stopped (kStallTrips trips without progress; a
+   nonzero word makes rt_render / rt_read_stats return RT_ERR_DEVICE).  Words 52..59
+   are the last stats launch's wave timeline (s_memrealtime, 100 MHz; cleared at
+   each stats launch, not accumulated; tools/timeline.py): ~earliest start, last
+   exit, ~earliest and last time a wave found the wave-tile queue drained, sum and
+   max of drain-to-exit, sum of start-to-exit, waves.  Not needed to render. */
 int rt_read_raw_stats(rt_scene* scene, uint64_t* out, uint32_t n);
 
 /* Sample chunking of the work units: a pixel's spp samples are

@@ -108,3 +108,34 @@ def test_kernel_instance_from_tuning():
         prices, row = b.class_prices(b.kernel_instance(t))
         assert prices and row in ("C2", "C3", "tri_f64")
     assert b.class_prices("path_kernel<false, false, 3, false, 3, false>") == (None, None)
+
+
+def test_dist_timeout_outlasts_the_pmc_passes():
+    """Under torchrun ranks 1..N-1 wait in init_process_group while rank 0 runs its
+    rocprofv3 --pmc children: the group's timeout covers every child's
+    own limit, and both backends are given it."""
+    b = _bench()
+    assert b.DIST_TIMEOUT_S > len(b.PMC_PASSES) * b.PMC_CHILD_TIMEOUT_S
+    src = open(os.path.join(HERE, "..", "bench.py")).read()
+    assert 'init_process_group("nccl", device_id=dev, timeout=pg_timeout)' in src
+    assert 'init_process_group("gloo", timeout=pg_timeout)' in src
+
+
+def test_cpu_baseline_without_any_oracle_build(monkeypatch):
+    """a host where neither oracle build works keeps the GPU line: the
+    baseline's value is None and the per-build errors are reported."""
+    import sys
+    import types
+    b = _bench()
+    fake = types.ModuleType("oracle")
+
+    class Boom:
+        def __init__(self, *a, **k):
+            raise RuntimeError("no compiler")
+
+    fake.OracleScene = Boom
+    monkeypatch.setitem(sys.modules, "oracle", fake)
+    out = b.cpu_baseline(None, None, 1.0)
+    assert out["value"] is None and out["value_build"] is None
+    assert set(out["builds"]) == {"native", "portable"}
+    assert all("no compiler" in v["error"] for v in out["builds"].values())

@@ -55,3 +55,23 @@ def test_forced_chunk_spp_is_bounded(cornell, rt):
         assert st["paths"] == 16 * 16 * 8 and np.isfinite(img).all()
     finally:
         s.set_tuning()
+
+
+def test_tail_split_reports_the_resolved_form(cornell, rt):
+    """get_tuning reports the split the last frame resolved to — 1 when the
+    split cannot apply (one sample run of >= 65536 rows) — and the setting before any
+    render since set_tuning."""
+    desc, params, s = cornell
+    try:
+        s.set_tuning(tail_split=8, chunk_spp=65536)
+        assert s.tuning()["tail_split"] == 8
+        p = params.replace(width=16, height=16, spp=65536, ray_depth=1)
+        assert s.sample_chunks(p) == (1, 65536)
+        img, _, st = s.generate_image(p, stats=True)
+        assert st["paths"] == 16 * 16 * 65536 and np.isfinite(img).all()
+        assert s.tuning()["tail_split"] == 1
+        s.set_tuning(tail_split=8)
+        s.generate_image(params.replace(width=16, height=16, spp=8), stats=True)
+        assert s.tuning()["tail_split"] == 8  # resolved: a small frame is all tail wave-tiles
+    finally:
+        s.set_tuning()

@@ -14,7 +14,8 @@ from conftest import REPO
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
-ARGS = ["--workload", "C1", "--steps", "1", "--warmup", "0", "--no-pmc", "--no-cpu-baseline"]
+BASE = ["--workload", "C1", "--steps", "1", "--warmup", "0", "--no-cpu-baseline"]
+ARGS = BASE + ["--no-pmc"]
 
 
 def _line(out):
@@ -23,9 +24,9 @@ def _line(out):
     return json.loads(lines[-1])
 
 
-def _run(extra, timeout=240):
+def _run(extra, timeout=240, args=ARGS):
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
-    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *ARGS, *extra], capture_output=True,
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args, *extra], capture_output=True,
                           text=True, timeout=timeout, env=env)
 
 
@@ -46,3 +47,19 @@ def test_bench_gpus2_nccl_refuses_one_gpu():
     r = _run(["--gpus", "2"])
     assert r.returncode != 0
     assert "visible GPU" in r.stdout + r.stderr
+
+
+def test_bench_gpus2_gloo_with_pmc_passes():
+    """The driver's N>1 command keeps its PMC passes: rank 0 runs its
+    rocprofv3 --pmc children while rank 1 waits in init_process_group (timeout =
+    bench.DIST_TIMEOUT_S); the line then carries rank 0's roofline (VALU and HBM), the
+    world it saw and the one-rank digest."""
+    one = _run([])
+    assert one.returncode == 0, one.stderr[-2000:]
+    two = _run(["--gpus", "2", "--dist-backend", "gloo"], timeout=600, args=BASE)
+    assert two.returncode == 0, two.stderr[-2000:]
+    a, b = _line(one.stdout), _line(two.stdout)
+    assert b["world_size_seen"] == 2 and b["image_sha256"] == a["image_sha256"]
+    r = b["roofline"]
+    assert r["frac"] is not None and r["frac"] > 0, r
+    assert r["hbm"]["frac"] > 0 and r["traffic"] > 0

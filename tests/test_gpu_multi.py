@@ -69,6 +69,10 @@ def test_replicas_filled_from_device0(rt, cornell, atrium):
             assert infos[i]["device_bytes"] == infos[0]["device_bytes"] > 0
             assert infos[i]["bvh_nodes"] == infos[0]["bvh_nodes"]
             assert infos[i]["upload_ms"] > 0.0
+        # the content hashes rt_multi_create compared: every replica's
+        # equals devices[0]'s, and a scene built from the host alone
+        hs = [m.scene_checksum(i) for i in range(3)]
+        assert hs[0] == hs[1] == hs[2] == rt.Scene(desc).checksum()
         img, _, _ = m.generate_image(params)
         assert np.array_equal(img, ref)
         m.close()
@@ -125,3 +129,11 @@ def test_multi_scene_handles(rt, cornell):
     with pytest.raises(rt.RtError):  # hit-id dumps stay rt_render's
         m.generate_image(cornell[1].replace(flags=rt.RT_FLAG_HIT_IDS))
     m.close()
+
+
+def test_checksum_tells_scenes_apart(rt, cornell, atrium):
+    """rt_scene_checksum is a function of the scene's device bytes: the same description
+    hashes equal on every build, different scenes differ."""
+    a, b = cornell[0], atrium[0]
+    assert rt.Scene(a).checksum() == rt.Scene(a).checksum()
+    assert rt.Scene(a).checksum() != rt.Scene(b).checksum()

@@ -34,7 +34,7 @@ def sink(rt, orc, scene_text):
 FORM = {}
 
 
-@pytest.fixture(autouse=True, params=["fused", "resume", "resume_eager", "resume_f64", "general"])
+@pytest.fixture(autouse=True, params=["fused", "resume", "resume_eager", "resume_f64", "resume_pair", "general"])
 def segment_form(request):
     """Every test runs both path-kernel segment forms: fused (whole closest-hit
     query, then shading) and resumable (triangle traversal suspended while few
@@ -46,13 +46,17 @@ def segment_form(request):
     host would pick a shape-only or triangle-only one (api.cpp path_kinds).
     The resumable forms read a glTF scene's triangle BVH in its compact layout
     (f32 child boxes and vertices, exact copies: api.cpp path_compact);
-    "resume_f64" forces the f64 layout in the same kernel."""
+    "resume_f64" forces the f64 layout in the same kernel; "resume_pair" the compact
+    layout's pair lines (two BVH levels per line, rt_tuning.compact = 2) where the scene
+    has them (RT_LAYOUT_PAIR_NODES), else the compact one."""
     FORM.clear()
     FORM["resume"] = 1 if request.param.startswith("resume") else 0
     if request.param == "resume_eager":
         FORM.update(suspend_lanes=64, leaf_lanes=1)
     if request.param == "resume_f64":
         FORM["compact"] = 0
+    if request.param == "resume_pair":
+        FORM["compact"] = 2
     if request.param == "general":
         FORM["kinds"] = 3
     yield request.param
@@ -61,7 +65,10 @@ def segment_form(request):
 
 def form(scene, **extra):
     """Apply the current test's kernel form (+ extra fields) to a device scene."""
-    scene.set_tuning(**{**FORM, **extra})
+    t = {**FORM, **extra}
+    if t.get("compact") == 2 and not scene.info()["layout_flags"] & 0x4:
+        t.pop("compact")  # no pair layout (no compact triangle BVH): the scene's own form
+    scene.set_tuning(**t)
     return scene
 
 
@@ -562,6 +569,26 @@ def test_deep_stack_and_big_leaf_render(rt, orc):
                         cam_forward=tuple(f), cam_up=tuple(u), fov=0.9)
     img, _, st = _compare(g, o, p, waves=4)
     assert st["tri_tests"] > 0 and st["shaded_hits"] > 0
+
+
+def test_progress_guard_single_row_tiles(rt, orc, segment_form):
+    """the stats instance's progress guard (render.h kStatStall) on the
+    regime of the round-5 livelock — one-row wave-tiles (chunk_spp 1), the queue's tail
+    in 8 parts, a deep BVH with a spilling stack, the resumable forms: every wave must
+    finish (a stalled wave makes rt_render fail, api.cpp copy_stats), and the frame is the
+    oracle's bit for bit."""
+    if not segment_form.startswith("resume"):
+        pytest.skip("the guard's regime is the resumable kernel's suspend test")
+    desc = _deep_chain(rt)
+    desc.tri_vertices = desc.tri_vertices.astype(np.float32).astype(np.float64)
+    g, o = rt.Scene(desc), orc.OracleScene(desc)
+    f = np.array([0.0, -0.4, 1.0]) / np.sqrt(1.16)
+    u = np.array([0.0, 1.0, 0.4]) / np.sqrt(1.16)
+    p = rt.RenderParams(width=96, height=64, spp=48, ray_depth=3, cam_position=(0.0, 0.5, -1.0),
+                        cam_forward=tuple(f), cam_up=tuple(u), fov=0.9, seed=21)
+    _, _, st = _compare(g, o, p, waves=4, chunk_spp=1, tail_split=8)
+    assert g.sample_chunks(p) == (48, 1) and g.tuning()["tail_split"] == 8
+    assert g.read_raw_stats(15)[14] == 0 and st["paths"] == 96 * 64 * 48
 
 
 def test_deep_stack_and_big_leaf_compact_trace(rt, orc):

@@ -30,6 +30,19 @@ for s in $STEPS; do
     dist2) # the N=2 bench path (PMC children, tile shares, one gather, max-over-ranks) as a gloo rehearsal
       run bench_dist2 900 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
         --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --dist-backend gloo || exit 1 ;;
+    rehearse8)  # the driver's exact N=8 command, PMC passes on, all 8 gloo ranks on this one GPU
+      run bench_rehearsal_gloo8_pmc 900 $B --gpus 8 --dist-backend gloo || exit 1 ;;
+    wr2|wr3|wr5)  # where the writes come from: L2->fabric write requests by size, then the store
+      # instruction mix (VMEM / FLAT incl. scratch) — $WR_LIB (default the product), $WR_SPP
+      w=C${s#wr}
+      RT_AMD_LIB=${WR_LIB:-$PWD/cpu-raytracing-rt_amd/build/librt_amd.so} run wreq_$w 600 rocprofv3 --pmc \
+        TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_WRITE_sum TCC_EA0_WRREQ_DRAM_sum --output-format csv \
+        -d "$OUT/wreq_$w" -o run -- $B --workload $w --steps 1 --warmup 0 --no-cpu-baseline --no-pmc \
+        ${WR_SPP:+--spp $WR_SPP} || exit 1
+      RT_AMD_LIB=${WR_LIB:-$PWD/cpu-raytracing-rt_amd/build/librt_amd.so} run wins_$w 600 rocprofv3 --pmc \
+        SQ_INSTS_VMEM_WR SQ_INSTS_FLAT SQ_INSTS_VMEM_RD SQ_INSTS_SMEM SQ_WAVES SQ_INSTS_LDS SQ_ACTIVE_INST_FLAT \
+        TCP_TCC_WRITE_REQ_sum --output-format csv -d "$OUT/wins_$w" -o run \
+        -- $B --workload $w --steps 1 --warmup 0 --no-cpu-baseline --no-pmc ${WR_SPP:+--spp $WR_SPP} || exit 1 ;;
     c2)    run bench_c2 600 $B --workload C2 --steps 3 --warmup 1 || exit 1 ;;
     c3)    run bench_c3 600 $B --workload C3 --steps 3 --warmup 1 || exit 1 ;;
     c5)    run bench_c5 900 $B --workload C5 --steps 2 --warmup 1 || exit 1 ;;

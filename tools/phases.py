@@ -21,7 +21,7 @@ NAMES = ["assign", "intersect", "light_sample", "light_pdf", "segment", "commit"
          "rng_wave_refills", "rng_lane_refills",
          "w_intersect", "w_light_sample", "w_light_pdf", "w_segment", "w_commit",
          "isect_planes", "isect_boxes", "isect_ellipsoids", "isect_triangles", "isect_materialise",
-         "inner_wave_iters", "inner_lane_iters", "live_lane_iters", "rng_fallback_wave", "rng_fallback_lane",
+         "inner_wave_iters", "inner_lane_iters", "live_lane_iters", "idle_window_lanes", "idle_drained_lanes",
          "push_lane", "push_global", "pop_global", "leaf_cycles", "inner_cycles", "pop_cycles", "step_cycles",
          "inner_uniform_waves"]
 rt = load_package()
@@ -53,7 +53,9 @@ print(json.dumps({"workload": wl, "spp": spp, "segments": st["segments"],
                   "leaf_loop_util": ph["leaf_lane_tests"] / max(1, 64 * ph["leaf_wave_trips"]),
                   "rng_refill_util": ph["rng_lane_refills"] / max(1, 64 * ph["rng_wave_refills"]),
                   "rng_wave_refills_per_segment": ph["rng_wave_refills"] * 64 / max(1, st["segments"]),
-                  "rng_fallback_share": ph["rng_fallback_wave"] / max(1, ph["rng_wave_refills"]),
+                  # lanes without a path per path-loop trip: held by the commit window / queue drained
+                  "idle_window_frac": ph["idle_window_lanes"] / max(1, st["wave_steps"]),
+                  "idle_drained_frac": ph["idle_drained_lanes"] / max(1, st["wave_steps"]),
                   "stack_pushes_per_segment": ph["push_lane"] / max(1, st["segments"]),
                   "global_push_share": ph["push_global"] / max(1, ph["push_lane"]),
                   "global_stack_bytes": 12 * (ph["push_global"] + ph["pop_global"]),
