@@ -331,8 +331,12 @@ bool path_compact(const rt_scene* s) {
     return s->tune.compact != 0 && s->dev.tris.cnodes && path_waves(s) == 4 && path_resume(s) && path_kinds(s) == 2;
 }
 // The pair layout over the compact nodes (rt_layout.h kPairFloats, render.hip trav_step
-// PAIR: two BVH levels per dependent line): rt_tuning.compact = 2.
-bool path_pairs(const rt_scene* s) { return s->tune.compact == 2 && s->dev.tris.pnodes && path_compact(s); }
+// PAIR: two BVH levels per dependent line), whenever the scene has it (auto, or
+// rt_tuning.compact = 2; 1 forces the 64-B compact nodes): C3 -1.3%, C5 -1.9% per frame,
+// the same image (profiles/r06/bench_C*_compact_*.log).
+bool path_pairs(const rt_scene* s) {
+    return (s->tune.compact == -1 || s->tune.compact == 2) && s->dev.tris.pnodes && path_compact(s);
+}
 
 
 

@@ -373,14 +373,13 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
         asm volatile("" ::"v"(b0.x), "v"(b0.y), "v"(b0.z), "v"(b0.w), "v"(b1.x), "v"(b1.y), "v"(b1.z), "v"(b1.w),
                      "v"(b2.x), "v"(b2.y), "v"(b2.z), "v"(b2.w), "v"(bw.z), "v"(bw.w));  // one batch: see node_boxes
         PH_COUNT(kPhInnerWave, kPhInnerLane);
-        // half: A = (x0.xyz | x0.w x1.xy), B = (x1.zw x2.x | x2.yzw); a leaf child's box is A
+        // half: A = (x0.xyz | x0.w x1.xy), B = (x1.zw x2.x | x2.yzw); a child's box is A u B
+        // (a leaf child's half holds its box twice)
         const bool la = aw.w & kPairLeaf, lb = bw.w & kPairLeaf;
-        const float lmnx = la ? a0.x : fminf(a0.x, a1.z), lmny = la ? a0.y : fminf(a0.y, a1.w),
-                    lmnz = la ? a0.z : fminf(a0.z, a2.x), lmxx = la ? a0.w : fmaxf(a0.w, a2.y),
-                    lmxy = la ? a1.x : fmaxf(a1.x, a2.z), lmxz = la ? a1.y : fmaxf(a1.y, a2.w);
-        const float rmnx = lb ? b0.x : fminf(b0.x, b1.z), rmny = lb ? b0.y : fminf(b0.y, b1.w),
-                    rmnz = lb ? b0.z : fminf(b0.z, b2.x), rmxx = lb ? b0.w : fmaxf(b0.w, b2.y),
-                    rmxy = lb ? b1.x : fmaxf(b1.x, b2.z), rmxz = lb ? b1.y : fmaxf(b1.y, b2.w);
+        const float lmnx = fminf(a0.x, a1.z), lmny = fminf(a0.y, a1.w), lmnz = fminf(a0.z, a2.x),
+                    lmxx = fmaxf(a0.w, a2.y), lmxy = fmaxf(a1.x, a2.z), lmxz = fmaxf(a1.y, a2.w);
+        const float rmnx = fminf(b0.x, b1.z), rmny = fminf(b0.y, b1.w), rmnz = fminf(b0.z, b2.x),
+                    rmxx = fmaxf(b0.w, b2.y), rmxy = fmaxf(b1.x, b2.z), rmxz = fmaxf(b1.y, b2.w);
         C.aabb(2);
         double lt = 0.0, rt2 = 0.0;
         const bool lh = slab_c<SLAB>(lmnx, lmny, lmnz, lmxx, lmxy, lmxz, o, d, rc, fast, lt);

@@ -83,7 +83,7 @@ constexpr uint32_t kLeafBlock = 32;  // floats per 128-B line
 //   floats 0..5  box A, 6..11 box B, then words 12 A's word, 13 B's word, 14 K's own
 //   word (its child word in c), 15 flags.
 // K internal: A / B = K's children's boxes and words (what a visit of K tests); K's own
-// box is their union.  K a leaf (flags kPairLeaf): A = K's box.  A visit of c reads
+// box is their union.  K a leaf (flags kPairLeaf): A = B = K's box (the union again).  A visit of c reads
 // c's line, tests both children and can visit the near child K from the same line:
 // two BVH levels per dependent load.  Slot indices are the compact ones.
 constexpr uint32_t kPairFloats = 32, kPairHalf = 16;

@@ -319,7 +319,8 @@ bool f32_exact3(V3 v) { return f32_exact(v.x) && f32_exact(v.y) && f32_exact(v.z
 // tests — or K's own box when it is a leaf.  A visit of c then takes K's box as the union
 // of K's children's boxes (exact: a node's box is the union of its primitives' boxes,
 // bvh.rs:56-62, so the f32 min/max of the two children's boxes is the same box) and can
-// go on to visit the near child K from the same line.  Built only when that union
+// go on to visit the near child K from the same line (a leaf K's box is stored as both
+// boxes, so the union is its box too).  Built only when that union
 // reproduces every internal child's box; otherwise left empty (the compact form stays).
 void build_pairs(HostBvhArrays& out, size_t n_int) {
     const std::vector<DevNodeC>& cn = out.cnodes;
@@ -331,9 +332,12 @@ void build_pairs(HostBvhArrays& out, size_t n_int) {
             const float* mn = side ? cn[c].rmin : cn[c].lmin;
             const float* mx = side ? cn[c].rmax : cn[c].lmax;
             uint32_t words[4] = {0u, 0u, w, 0u};
-            if (w & (kPackedLeaf | kLeafRef)) {  // a leaf child: its own box
-                std::memcpy(h, mn, 3 * sizeof(float));
-                std::memcpy(h + 3, mx, 3 * sizeof(float));
+            if (w & (kPackedLeaf | kLeafRef)) {  // a leaf child: its own box, as A and as B
+                // (so the device's union of A and B is the box without a select)
+                for (int k = 0; k < 2; ++k) {
+                    std::memcpy(h + 6 * k, mn, 3 * sizeof(float));
+                    std::memcpy(h + 6 * k + 3, mx, 3 * sizeof(float));
+                }
                 words[3] = kPairLeaf;
             } else {  // an internal child K = slot w: the boxes its visit tests, its words
                 const DevNodeC& k = cn[w];

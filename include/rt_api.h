@@ -197,7 +197,8 @@ typedef struct rt_scene_info {
 #define RT_LAYOUT_LQ_SKIP      0x2u
 /* RT_LAYOUT_PAIR_NODES: the compact triangle BVH also has its pair layout (one 128-B
    line per inner node holding what a visit of either child tests, so a descent reads
-   one line per two levels), selected by rt_tuning.compact = 2 */
+   one line per two levels), which the resumable kernel reads when it is
+   there (rt_tuning.compact auto or 2) */
 #define RT_LAYOUT_PAIR_NODES   0x4u
 int rt_scene_get_info(const rt_scene* scene, rt_scene_info* out);
 /* Content hash of the scene's device arrays (BVHs, records, materials; not the
@@ -224,8 +225,9 @@ typedef struct rt_tuning {
     uint32_t chunk_spp;      /* 0 the frame's rule (rt_sample_chunks); else the sample run length,
                                 raised if need be to <= 64 runs and <= 4 GiB of partial sums
                                 (rt_scene_sample_chunks reports the run length used)                    */
-    int32_t  compact;        /* -1 auto (1 when the scene has it: RT_LAYOUT_COMPACT_TRIS); 0 the f64
-                                triangle-BVH layout; 1 the compact one (triangle-only resumable kernel;
+    int32_t  compact;        /* -1 auto (2 when the scene has RT_LAYOUT_PAIR_NODES, else 1 when it
+                                has RT_LAYOUT_COMPACT_TRIS); 0 the f64 triangle-BVH layout; 1 the
+                                compact one with 64-B nodes (triangle-only resumable kernel;
                                 RT_ERR_UNSUPPORTED on a scene without RT_LAYOUT_COMPACT_TRIS); 2 the
                                 compact one with its pair layout (RT_LAYOUT_PAIR_NODES)               */
     uint32_t tail_split;     /* 0 auto (8); 1 every wave-tile whole; 2..8: the queue's last wave-tiles

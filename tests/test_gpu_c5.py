@@ -28,8 +28,9 @@ def test_c5_full_frame(rt, orc):
     scene = rt.Scene(desc)
     info = scene.info()
     assert info["layout_flags"] & 1  # f32 glTF positions: the compact triangle layout exists
+    assert info["layout_flags"] & 4  # ... with its pair layout, which the resumable kernel reads
     t = scene.tuning()
-    assert (t["waves"], t["resume"], t["kinds"], t["compact"]) == (4, 1, 2, 1)
+    assert (t["waves"], t["resume"], t["kinds"], t["compact"]) == (4, 1, 2, 2)
     assert (t["suspend_lanes"], t["leaf_lanes"]) == (48, 28)  # streamed-BVH thresholds (render.h)
     chunks, chunk_spp = scene.sample_chunks(params)
 
@@ -38,6 +39,13 @@ def test_c5_full_frame(rt, orc):
     assert np.array_equal(prod, img), f"product vs stats instance: max |d| {np.abs(prod - img).max()}"
     assert np.isfinite(img).all() and (img >= 0).all() and img.max() > 0
     assert st["paths"] == W * H * spp and st["tri_tests"] > st["segments"]
+    # the compact layout's 64-B nodes (one BVH level per line) give the same frame and work
+    scene.set_tuning(compact=1)
+    img1, _, st1 = scene.generate_image(params, stats=True)
+    assert np.array_equal(img1, img)
+    for k in ("paths", "segments", "aabb_tests", "tri_tests", "shaded_hits", "light_queries", "light_hits"):
+        assert st1[k] == st[k], k
+    scene.set_tuning()
 
     threads, _ = bench.cpu_share()
     osc = orc.OracleScene(desc)  # the restated reference builder, once

@@ -52,10 +52,11 @@ def test_full_frame_rows_match_oracle(rt, orc, name, rows):
         assert o_st["paths"] == params.width * params.spp
     if name == "C3":
         # the other segment form renders the identical frame (C3 picks the resumable one)
-        # C3 runs the resumable kernel on the compact triangle layout; the f64 layout in the
-        # same kernel and the fused form render the identical frame and counters
-        assert scene.tuning()["resume"] == 1 and scene.tuning()["compact"] == 1
-        for tune in (dict(compact=0), dict(resume=0)):
+        # C3 runs the resumable kernel on the compact triangle layout's pair lines; its 64-B
+        # nodes, the f64 layout in the same kernel and the fused form render the identical
+        # frame and counters
+        assert scene.tuning()["resume"] == 1 and scene.tuning()["compact"] == 2  # pair layout
+        for tune in (dict(compact=1), dict(compact=0), dict(resume=0)):
             scene.set_tuning(**tune)
             img2, _, st2 = scene.generate_image(params, stats=True)
             assert np.array_equal(img, img2), tune

@@ -49,7 +49,9 @@ def test_hairball(hairball, segment_form):
     assert st["tri_tests"] > 0 and st["shaded_hits"] > 0
     # glTF positions are f32: the compact triangle layout exists and the resumable forms read it
     assert g.info()["layout_flags"] & 1
-    assert g.tuning()["compact"] == (1 if segment_form in ("resume", "resume_eager") else 0)
+    assert g.info()["layout_flags"] & 4  # and its pair layout (every inner box is its children's union)
+    want = {"resume": 2, "resume_eager": 2, "resume_c64": 1}.get(segment_form, 0)
+    assert g.tuning()["compact"] == want
 
 
 def test_room(room):

@@ -34,7 +34,7 @@ def sink(rt, orc, scene_text):
 FORM = {}
 
 
-@pytest.fixture(autouse=True, params=["fused", "resume", "resume_eager", "resume_f64", "resume_pair", "general"])
+@pytest.fixture(autouse=True, params=["fused", "resume", "resume_eager", "resume_f64", "resume_c64", "general"])
 def segment_form(request):
     """Every test runs both path-kernel segment forms: fused (whole closest-hit
     query, then shading) and resumable (triangle traversal suspended while few
@@ -46,17 +46,17 @@ def segment_form(request):
     host would pick a shape-only or triangle-only one (api.cpp path_kinds).
     The resumable forms read a glTF scene's triangle BVH in its compact layout
     (f32 child boxes and vertices, exact copies: api.cpp path_compact);
-    "resume_f64" forces the f64 layout in the same kernel; "resume_pair" the compact
-    layout's pair lines (two BVH levels per line, rt_tuning.compact = 2) where the scene
-    has them (RT_LAYOUT_PAIR_NODES), else the compact one."""
+    "resume_f64" forces the f64 layout in the same kernel; the auto forms read the compact
+    layout's pair lines (two BVH levels per line, RT_LAYOUT_PAIR_NODES) where the scene has
+    them, and "resume_c64" forces the compact layout's 64-B nodes (rt_tuning.compact = 1)."""
     FORM.clear()
     FORM["resume"] = 1 if request.param.startswith("resume") else 0
     if request.param == "resume_eager":
         FORM.update(suspend_lanes=64, leaf_lanes=1)
     if request.param == "resume_f64":
         FORM["compact"] = 0
-    if request.param == "resume_pair":
-        FORM["compact"] = 2
+    if request.param == "resume_c64":
+        FORM["compact"] = 1
     if request.param == "general":
         FORM["kinds"] = 3
     yield request.param
@@ -66,8 +66,8 @@ def segment_form(request):
 def form(scene, **extra):
     """Apply the current test's kernel form (+ extra fields) to a device scene."""
     t = {**FORM, **extra}
-    if t.get("compact") == 2 and not scene.info()["layout_flags"] & 0x4:
-        t.pop("compact")  # no pair layout (no compact triangle BVH): the scene's own form
+    if t.get("compact") == 1 and not scene.info()["layout_flags"] & 0x1:
+        t.pop("compact")  # no compact triangle BVH: the scene's own form
     scene.set_tuning(**t)
     return scene
 

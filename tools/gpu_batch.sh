@@ -38,11 +38,21 @@ for s in $STEPS; do
       RT_AMD_LIB=${WR_LIB:-$PWD/cpu-raytracing-rt_amd/build/librt_amd.so} run wreq_$w 600 rocprofv3 --pmc \
         TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_WRITE_sum TCC_EA0_WRREQ_DRAM_sum --output-format csv \
         -d "$OUT/wreq_$w" -o run -- $B --workload $w --steps 1 --warmup 0 --no-cpu-baseline --no-pmc \
-        ${WR_SPP:+--spp $WR_SPP} || exit 1
+        ${WR_SPP:+--spp $WR_SPP} ${WR_TUNE:+--tune $WR_TUNE} || exit 1
       RT_AMD_LIB=${WR_LIB:-$PWD/cpu-raytracing-rt_amd/build/librt_amd.so} run wins_$w 600 rocprofv3 --pmc \
         SQ_INSTS_VMEM_WR SQ_INSTS_FLAT SQ_INSTS_VMEM_RD SQ_INSTS_SMEM SQ_WAVES SQ_INSTS_LDS SQ_ACTIVE_INST_FLAT \
         TCP_TCC_WRITE_REQ_sum --output-format csv -d "$OUT/wins_$w" -o run \
-        -- $B --workload $w --steps 1 --warmup 0 --no-cpu-baseline --no-pmc ${WR_SPP:+--spp $WR_SPP} || exit 1 ;;
+        -- $B --workload $w --steps 1 --warmup 0 --no-cpu-baseline --no-pmc ${WR_SPP:+--spp $WR_SPP} \
+        ${WR_TUNE:+--tune $WR_TUNE} || exit 1 ;;
+    hit3|hit5)  # L1 (TCP) and L2 (TCC) hit rates of the path kernel's loads, with --tune $TUNE
+      w=C${s#hit}
+      run tcphit_${w}_$(echo "$TUNE" | tr ',=' '__') 600 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum \
+        TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum --output-format csv \
+        -d "$OUT/tcphit_${w}_$(echo "$TUNE" | tr ',=' '__')" -o run -- $B --workload $w --steps 1 --warmup 0 \
+        --no-cpu-baseline --no-pmc --spp ${HIT_SPP:-16} --tune "$TUNE" || exit 1 ;;
+    tc3|tc5)  # the full-frame bench of C3 / C5 with --tune $TUNE (a kernel form the host does not pick yet)
+      w=C${s#tc}
+      run bench_${w}_$(echo "$TUNE" | tr ',=' '__') 900 $B --workload $w --steps 2 --warmup 1 --tune "$TUNE" || exit 1 ;;
     c2)    run bench_c2 600 $B --workload C2 --steps 3 --warmup 1 || exit 1 ;;
     c3)    run bench_c3 600 $B --workload C3 --steps 3 --warmup 1 || exit 1 ;;
     c5)    run bench_c5 900 $B --workload C5 --steps 2 --warmup 1 || exit 1 ;;
