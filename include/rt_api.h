@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RT_API_VERSION 5
+#define RT_API_VERSION 6
 
 typedef enum rt_error {
     RT_OK = 0,
@@ -235,7 +235,7 @@ typedef struct rt_tuning {
                                 consecutive sample rows and summed in sample order after the launch
                                 (the same image: DESIGN.md section 5 "per-launch tail")            */
     /* Version 5 replaced version 4's last field (`sorted`, the regrouped-shading kernel) with
-       tail_split.  Auto is 0 for the unsigned fields and -1 for the signed ones (resume,
+       tail_split; version 6 added compact = 2 (the same struct).  Auto is 0 for the unsigned fields and -1 for the signed ones (resume,
        compact): a zero-initialised struct is not all-auto.  NULL restores every field to auto. */
 } rt_tuning;
 /* NULL restores every field to auto.  Fields out of range -> RT_ERR_INVALID. */

@@ -30,7 +30,7 @@ def test_header_symbols_exported(rt):
 
 
 def test_version_and_errors(rt):
-    assert rt.lib().rt_api_version() == 5
+    assert rt.lib().rt_api_version() == 6
     with pytest.raises(rt.RtError) as e:
         rt.parse_scene("NEW_PRIMITIVE\nBOX 1 2\n")
     assert e.value.code == -4
