@@ -56,6 +56,48 @@ static std::string check_bvh(const rt::HostBvhArrays& b) {
     return "";
 }
 
+// The pair layout over the compact nodes (scene_build.cpp build_pairs, rt_layout.h
+// kPairFloats): every half is its child's record — a leaf child's box twice, an internal
+// child's compact node — and the union of its two boxes is the child's box as the
+// compact parent stores it (what the device takes as the box).  Counts checked lines.
+static size_t g_pair_lines = 0, g_pair_bvhs = 0;
+static std::string check_pairs(const rt::HostBvhArrays& b) {
+    if (b.pnodes.empty()) return "";
+    if (b.pnodes.size() % rt::kPairFloats) return "pair array not whole lines";
+    const size_t n_int = b.pnodes.size() / rt::kPairFloats;
+    const auto& cn = b.cnodes;
+    if (cn.size() < n_int) return "more pair lines than compact slots";
+    auto same = [](const float* a, const float* x, int n) { return std::memcmp(a, x, n * sizeof(float)) == 0; };
+    for (size_t c = 0; c < n_int; ++c) {
+        if (cn[c].count != 0) return "pair line for a leaf slot";
+        for (int side = 0; side < 2; ++side) {
+            const float* h = &b.pnodes[c * rt::kPairFloats + side * rt::kPairHalf];
+            uint32_t w[4];
+            std::memcpy(w, h + 12, sizeof(w));
+            const uint32_t cw = side ? cn[c].rw : cn[c].lw;
+            const float* mn = side ? cn[c].rmin : cn[c].lmin;
+            const float* mx = side ? cn[c].rmax : cn[c].lmax;
+            if (w[2] != cw) return "pair half: wrong own word";
+            if (cw & (rt::kPackedLeaf | rt::kLeafRef)) {
+                if (w[3] != rt::kPairLeaf || !same(h, mn, 3) || !same(h + 3, mx, 3) || !same(h + 6, h, 6))
+                    return "pair half: leaf box";
+            } else {
+                if (w[3] != 0 || cw >= n_int) return "pair half: internal child out of range";
+                const rt::DevNodeC& k = cn[cw];
+                if (!same(h, k.lmin, 3) || !same(h + 3, k.lmax, 3) || !same(h + 6, k.rmin, 3) ||
+                    !same(h + 9, k.rmax, 3) || w[0] != k.lw || w[1] != k.rw)
+                    return "pair half: not the child's compact node";
+                for (int a = 0; a < 3; ++a)
+                    if (std::fmin(h[a], h[6 + a]) != mn[a] || std::fmax(h[3 + a], h[9 + a]) != mx[a])
+                        return "pair half: union is not the child's box";
+            }
+        }
+    }
+    g_pair_lines += n_int;
+    ++g_pair_bvhs;
+    return "";
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) {
         fprintf(stderr, "usage: harness OUT_DIR FILE...\n");
@@ -96,7 +138,8 @@ int main(int argc, char** argv) {
             for (const auto& b : hs.bvh) {
                 nodes += b.nodes.size();
                 prims += b.n_prims;
-                const std::string e = check_bvh(b);
+                std::string e = check_bvh(b);
+                if (e.empty()) e = check_pairs(b);
                 if (!e.empty()) bad = e;
             }
             if (!bad.empty()) {
@@ -123,6 +166,7 @@ int main(int argc, char** argv) {
     }
     double thr[255];
     printf("thresholds %d\n", rt_byte_thresholds(thr));
+    printf("pairs %zu %zu\n", g_pair_bvhs, g_pair_lines);
     printf("done\n");
     return 0;
 }

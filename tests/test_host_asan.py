@@ -54,6 +54,9 @@ def run(harness, out_dir, files, timeout=300):
     assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
     lines = r.stdout.splitlines()
     assert lines[-1] == "done"
+    # pair-layout lines the harness checked (check_pairs), over every input
+    pl = [ln.split() for ln in lines if ln.startswith("pairs ")]
+    run.pairs = (int(pl[-1][1]), int(pl[-1][2])) if pl else (0, 0)
     res = {}
     for ln in lines:
         parts = ln.split(" ", 2)
@@ -132,6 +135,7 @@ def test_host_parser_and_builder_fuzz(harness, tmp_path, scene_text):
         assert res[v] == "ok", (v, res[v])
     kinds = {k: list(res.values()).count(k) for k in set(res.values())}
     assert kinds.get("parse-error", 0) > 50 and kinds.get("ok", 0) > 100, kinds
+    assert run.pairs[0] > 0, "no scene built a pair layout (grid-exact triangles should)"
 
 
 def _gltf_mutations():
