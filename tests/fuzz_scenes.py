@@ -69,9 +69,12 @@ def _material(rng, lines, light_ok):
         lines.append("EMISSION " + _fmt(rng.uniform(0.5, 12.0, 3)))
 
 
-def random_scene(seed, width=None, height=None, spp=2, depth=None):
+def random_scene(seed, width=None, height=None, spp=2, depth=None, tri_only=False):
+    """tri_only: triangles on the grid and nothing else (no planes, no mesh rotation),
+    so the scene is triangle-only with every coordinate an exact f32 — the compact
+    triangle layout and its pair lines (rt_layout.h) apply."""
     rng = np.random.default_rng(seed)
-    grid = bool(rng.random() < 0.6)
+    grid = bool(rng.random() < 0.6) or tri_only
     w = width or int(rng.choice([8, 17, 24, 31, 64]))
     h = height or int(rng.choice([5, 12, 16, 40]))
     lines = [f"DIMENSIONS {w} {h}", f"SAMPLES {spp}", f"RAY_DEPTH {depth or int(rng.integers(1, 9))}",
@@ -80,10 +83,10 @@ def random_scene(seed, width=None, height=None, spp=2, depth=None):
              "CAMERA_RIGHT 1 0 0", "CAMERA_UP 0 1 0",
              "CAMERA_FORWARD " + _fmt([_g(rng, -0.25, 0.25), _g(rng, -0.25, 0.25), 1.0]),
              "CAMERA_FOV_X " + repr(float(rng.uniform(0.6, 1.4)))]
-    style = rng.integers(0, 3)  # 0 shapes only, 1 triangles (+ planes), 2 both
+    style = 1 if tri_only else rng.integers(0, 3)  # 0 shapes only, 1 triangles (+ planes), 2 both
     floor = -1.0
     # planes: an open room, axis-aligned or tilted
-    for k in range(int(rng.integers(0, 6))):
+    for k in range(0 if tri_only else int(rng.integers(0, 6))):
         lines.append("NEW_PRIMITIVE")
         ax = k % 3
         n = [0.0, 0.0, 0.0]
@@ -158,7 +161,7 @@ def random_scene(seed, width=None, height=None, spp=2, depth=None):
         for _ in range(int(rng.integers(0, 4))):  # exact duplicates: ties at every hit
             tris.append(list(tris[int(rng.integers(0, len(tris)))]))
         order = rng.permutation(len(tris))
-        mesh_q = _quat(rng) if rng.random() < 0.3 else None
+        mesh_q = _quat(rng) if rng.random() < 0.3 and not tri_only else None
         for k in order:
             lines.append("NEW_PRIMITIVE")
             lines.append("TRIANGLE " + _fmt(tris[k]))

@@ -43,6 +43,31 @@ def test_fuzz_render(rt, orc, seed):
             FORM.clear()
 
 
+# the compact layout's pair lines (two BVH levels per line, rt_layout.h kPairFloats) on
+# triangle-only grid scenes: ties (duplicates, shared edges and vertices, coplanar tiles),
+# flat leaf boxes and degenerate triangles through the 4-wave resumable kernel, which
+# reads the pair lines by default; the 64-B compact nodes and the eager form beside it
+PAIR_FORMS = {
+    "pair": dict(resume=1, waves=4),
+    "pair_eager": dict(resume=1, waves=4, suspend_lanes=64, leaf_lanes=1),
+    "compact64": dict(resume=1, waves=4, compact=1),
+}
+
+
+@pytest.mark.parametrize("seed", range(48))
+def test_fuzz_pair_layout(rt, orc, seed):
+    desc, params, g, o = _scenes(rt, orc, 5000 + seed, spp=4, depth=None if seed % 3 else 10, tri_only=True)
+    assert g.info()["layout_flags"] & 0x5 == 0x5  # the compact layout and its pair lines
+    for name, f in PAIR_FORMS.items():
+        FORM.clear()
+        FORM.update(f)
+        try:
+            _compare(g, o, params)
+            assert g.tuning()["compact"] == (1 if name == "compact64" else 2)
+        finally:
+            FORM.clear()
+
+
 def _aimed_rays(desc, rng, n):
     """Rays through mesh vertices and edge midpoints, from grid origins along grid
     directions (axis-parallel ones included): exact on a 1/16 grid, so each ray meets
