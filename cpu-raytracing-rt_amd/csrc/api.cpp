@@ -332,8 +332,9 @@ bool path_compact(const rt_scene* s) {
 }
 // The pair layout over the compact nodes (rt_layout.h kPairFloats, render.hip trav_step
 // PAIR: two BVH levels per dependent line), whenever the scene has it (auto, or
-// rt_tuning.compact = 2; 1 forces the 64-B compact nodes): C3 -1.3%, C5 -1.9% per frame,
-// the same image (profiles/r06/bench_C*_compact_*.log).
+// rt_tuning.compact = 2; 1 forces the 64-B compact nodes): C3 -3.5%, C5 -2.0% in
+// alternating runs, the same images and counters (profiles/r06/variants_pair2_C*.log,
+// DESIGN.md §4).
 bool path_pairs(const rt_scene* s) {
     return (s->tune.compact == -1 || s->tune.compact == 2) && s->dev.tris.pnodes && path_compact(s);
 }

@@ -308,11 +308,6 @@ void build_shape_bvh(const std::vector<ShapeItem>& items, HostBvhArrays& out) {
 bool f32_exact(double v) { return (double)(float)v == v || v != v; }
 bool f32_exact3(V3 v) { return f32_exact(v.x) && f32_exact(v.y) && f32_exact(v.z) && v.x == v.x && v.y == v.y && v.z == v.z; }
 
-// The compact layout (rt_layout.h DevNodeC + kTriC floats): built only when it
-// holds the same numbers — every child-box coordinate and every vertex a, b, c
-// is an exact f32 (glTF positions are f32: C3-C5; a custom TRIANGLE rotated by a
-// quaternion usually is not).  The device widens them back to f64 and rebuilds
-// ba = b - a, ca = c - a: the bits triangle_props computed from the same a, b, c.
 // Pair layout of the compact triangle BVH (rt_layout.h kPairFloats, DESIGN.md §4 "two
 // levels per line"): record c (one 128-B line per internal slot c) holds, for each child
 // K of c, K's children's boxes and words when K is internal — the boxes a visit of K
@@ -355,6 +350,11 @@ void build_pairs(HostBvhArrays& out, size_t n_int) {
     out.pnodes = std::move(pr);
 }
 
+// The compact layout (rt_layout.h DevNodeC + kTriC floats): built only when it
+// holds the same numbers — every child-box coordinate and every vertex a, b, c
+// is an exact f32 (glTF positions are f32: C3-C5; a custom TRIANGLE rotated by a
+// quaternion usually is not).  The device widens them back to f64 and rebuilds
+// ba = b - a, ca = c - a: the bits triangle_props computed from the same a, b, c.
 void build_compact(const HostBvh& h, const std::vector<TriItem>& items, HostBvhArrays& out) {
     for (const HostNode& n : h.nodes)
         if (!f32_exact3(n.box.min) || !f32_exact3(n.box.max)) return;
