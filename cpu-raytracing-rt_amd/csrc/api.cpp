@@ -903,8 +903,10 @@ int rt_intersect_rays_async(rt_scene* s, const double* d_rays, uint32_t n, rt_hi
     if (rc) return rc;
     if (!s->queue) HIP_TRY(hipMalloc(&s->queue, kQueueWords * sizeof(uint32_t)));
     HIP_TRY(ws_begin(s, st));
-    // the persistent form reads the compact triangle layout when the scene has it (rt_tuning.compact)
-    HIP_TRY(launch_trace(s->dev, d_rays, n, d_out, s->queue, s->spill_n, s->spill_t, grid, s->tune.compact != 0, st));
+    // the persistent form reads the compact triangle layout's pair lines, or its 64-B nodes, or the
+    // f64 layout, as rt_tuning.compact says (auto: the pair lines when the scene has them)
+    HIP_TRY(launch_trace(s->dev, d_rays, n, d_out, s->queue, s->spill_n, s->spill_t, grid,
+                         s->tune.compact == 0 ? 0 : (s->tune.compact == 1 ? 1 : 2), st));
     HIP_TRY(ws_end(s, st));
     return RT_OK;
 }

@@ -149,8 +149,9 @@ hipError_t path_grid(bool stats, bool hits, uint32_t waves, bool resume, int kin
 hipError_t launch_path(const DevScene& S, const KParams& P, const PathWork& W, double* out, int32_t* hit_ids,
                        unsigned long long* stats, hipStream_t st);
 hipError_t launch_reduce_chunks(const double* part, double* out, const KParams& P, hipStream_t st);
+// compact: 0 the f64 triangle layout, 1 the compact one, 2 its pair lines (when the scene has them)
 hipError_t launch_trace(const DevScene& S, const double* rays, uint32_t n, rt_hit* out, uint32_t* queue,
-                        uint32_t* spill_n, double* spill_t, uint32_t grid, bool compact, hipStream_t st);
+                        uint32_t* spill_n, double* spill_t, uint32_t grid, int compact, hipStream_t st);
 hipError_t trace_grid(uint32_t n, uint32_t* grid);
 #ifdef RT_WF_PROBE
 hipError_t launch_trace_tri(const DevScene& S, const double* rays, uint32_t n, rt_hit* out, uint32_t* queue,

@@ -1868,7 +1868,8 @@ RT_D void write_hit(rt_hit* __restrict__ out, uint32_t i, bool ok, const Hit& h,
     out[i] = r;
 }
 
-template <int WAVES, bool CMP = false>  // CMP: the triangle BVH's compact layout (trav_step)
+// CMP: the triangle BVH's compact layout, PAIR: its pair lines (trav_step)
+template <int WAVES, bool CMP = false, bool PAIR = false>
 __global__ __launch_bounds__(kWave, WAVES) void trace_kernel(DevScene S, const double* __restrict__ rays,
                                                              uint32_t n, rt_hit* __restrict__ out,
                                                              uint32_t* __restrict__ queue, uint32_t* spill_n,
@@ -1903,7 +1904,7 @@ __global__ __launch_bounds__(kWave, WAVES) void trace_kernel(DevScene S, const d
             }
         }
         const uint64_t lv2 = __ballot(q.T.live);
-        if (lv2) trav_step<3, 2, false, CMP>(S.tris, ps.o, ps.d, q.rc, q.fast, stk, C, q.T, lv2);
+        if (lv2) trav_step<3, 2, false, CMP, PAIR>(S.tris, ps.o, ps.d, q.rc, q.fast, stk, C, q.T, lv2);
         if (has && !q.T.live) {
             Hit h; uint32_t mat = 0; int32_t gid = 0;
             take_tri(q.best, q.T.valid, q.T.best, q.T.bu, q.T.bv, q.T.prim);
@@ -2159,10 +2160,13 @@ hipError_t launch_intersect(const DevScene& S, const double* rays, uint32_t n, r
 }
 // persistent batch intersect (trace_kernel): grid = resident waves, capped by the rays
 hipError_t launch_trace(const DevScene& S, const double* rays, uint32_t n, rt_hit* out, uint32_t* queue,
-                        uint32_t* spill_n, double* spill_t, uint32_t grid, bool compact, hipStream_t st) {
+                        uint32_t* spill_n, double* spill_t, uint32_t grid, int compact, hipStream_t st) {
     hipError_t e = hipMemsetAsync(queue, 0, kQueueWords * sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
-    if (compact && S.tris.cnodes)
+    if (compact == 2 && S.tris.pnodes)
+        hipLaunchKernelGGL((trace_kernel<4, true, true>), dim3(grid), dim3(kWave), 0, st, S, rays, n, out, queue,
+                           spill_n, spill_t);
+    else if (compact && S.tris.cnodes)
         hipLaunchKernelGGL((trace_kernel<4, true>), dim3(grid), dim3(kWave), 0, st, S, rays, n, out, queue, spill_n,
                            spill_t);
     else

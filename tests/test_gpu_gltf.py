@@ -86,10 +86,11 @@ def test_atrium_intersect_random(atrium):
     assert (gh["prim"] >= 0).mean() > 0.75   # open-roofed atrium: upward rays may escape
 
 
-@pytest.mark.parametrize("method,compact", [(0, -1), (1, -1), (1, 0)])
+@pytest.mark.parametrize("method,compact", [(0, -1), (1, -1), (1, 1), (1, 0)])
 def test_atrium_intersect_device(atrium, rt, method, compact):
     """Deep triangle BVH through both device batch kernels (the persistent one on the
-    compact triangle layout, and forced to the f64 one): the oracle's hits."""
+    compact layout's pair lines by default, on its 64-B nodes, and forced to the f64
+    layout): the oracle's hits."""
     desc, params, g, o = atrium
     g.set_tuning(compact=compact)
     rng = np.random.default_rng(14)

@@ -1,7 +1,7 @@
 """Batch closest-hit throughput on a bench scene: one-thread-per-ray vs the
 persistent traversal (rt_intersect_rays_async methods 0 and 1).
 
-usage: python tools/trace_bench.py WORKLOAD [N_RAYS]
+usage: [TRACE_COMPACT=-1|0|1] python tools/trace_bench.py WORKLOAD [N_RAYS]
 
 Rays: the scene's camera rays at the workload's resolution (one jittered ray per
 pixel), then diffuse bounce rays from their hits (cosine directions about the
@@ -42,6 +42,9 @@ def main():
     scene_file, W, H, spp, _ = bench.WORKLOADS[wl]
     desc, params = bench.load_workload(rt, scene_file, W, H, 1)
     scene = rt.Scene(desc)
+    # TRACE_COMPACT: the persistent form's triangle layout (rt_tuning.compact: -1 auto = the
+    # pair lines when the scene has them, 1 the 64-B compact nodes, 0 the f64 layout)
+    scene.set_tuning(compact=int(os.environ.get("TRACE_COMPACT", "-1")))
     c = params.to_c()
     rng = np.random.default_rng(7)
     # Camera::fuzzy_ray (camera.rs:48-55), normalised as raytrace.rs:9 does
