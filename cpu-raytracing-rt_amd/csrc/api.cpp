@@ -355,14 +355,17 @@ uint64_t bvh_hot_bytes(const rt_scene* s) {
 bool bvh_streamed(const rt_scene* s) { return bvh_hot_bytes(s) > kCacheBytes; }
 uint32_t path_suspend(const rt_scene* s) {
     if (s->tune.suspend_lanes) return s->tune.suspend_lanes;
+    if (path_compact(s)) return bvh_streamed(s) ? kSuspendCoopStreamed : kSuspendCoopCached;  // leaf_coop
     return bvh_streamed(s) ? kSuspendStreamed : kSuspendCached;
 }
 
 // Leaf batch of the resumable traversal (render.hip trav_step: lanes waiting at
 // leaves before the wave tests them), by the same cache criterion as the suspend
-// threshold (render.h kLeafCached / kLeafStreamed).  rt_tuning.leaf_lanes forces one.
+// threshold (render.h kLeafCached / kLeafStreamed; the compact layout's kernel, whose
+// small leaves are tested cooperatively, kLeafCoop*).  rt_tuning.leaf_lanes forces one.
 uint32_t path_leaf_batch(const rt_scene* s) {
     if (s->tune.leaf_lanes) return s->tune.leaf_lanes;
+    if (path_compact(s)) return bvh_streamed(s) ? kLeafCoopStreamed : kLeafCoopCached;
     return bvh_streamed(s) ? kLeafStreamed : kLeafCached;
 }
 

@@ -132,6 +132,16 @@ constexpr uint32_t kSuspendCached = 32, kSuspendStreamed = 48;
 // them): C3 16 -> 32 lanes 236.3 -> 227.1 ms, C5 16 -> 24 lanes 260.3 -> 249.5 ms at
 // 64 spp (profiles/r02/variants/variants_leaflanes*.log).
 constexpr uint32_t kLeafCached = 32, kLeafStreamed = 28;
+// The compact layout's kernel tests small leaves cooperatively (render.hip
+// leaf_coop: a leaf step costs one round per 64 records, not max(count) trips), so
+// it waits for fewer lanes at leaves and suspends later on a cached BVH. Round 6,
+// alternating runs (profiles/r06/variants_coop_grid*_C*.log): C3 at 64 spp
+// 24 / 16 173.4-174.1 ms (32 / 32 serial 177.1-177.5; 20 / 16 173.6, 24 / 12
+// 174.4, 16 / 12 174.8, 32 / 16 176.1, 40 / 16 179.4), C5 at 16 spp 48 / 12
+// 50.9-51.0 ms (48 / 28 serial 54.7-55.6; 44 / 12 50.9, 40 / 12 50.6-51.0,
+// 48 / 10 51.6, 48 / 14 51.3, 48 / 20 53.2, 56 / 12 52.8, 32 / 12 52.1).
+constexpr uint32_t kSuspendCoopCached = 24, kSuspendCoopStreamed = 48;
+constexpr uint32_t kLeafCoopCached = 16, kLeafCoopStreamed = 12;
 constexpr uint64_t kCacheBytes = 256ull << 20;  // MI355X Infinity Cache (MALL)
 constexpr uint64_t kDeepSceneNodes = 4096;  // BVH nodes above which the 4-wave kernel runs
 constexpr uint32_t kTailSplit = 8;                      // parts per tail wave-tile (api.cpp prepare_path)

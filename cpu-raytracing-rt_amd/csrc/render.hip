@@ -279,6 +279,74 @@ RT_D TriRec load_tri_c(const float* __restrict__ p) {
     return TriRec{A, v3(b.x, b.y, b.z) - A, v3(c.x, c.y, c.z) - A};
 }
 
+#ifndef RT_LEAF_SERIAL  // ablation build: every leaf by the serial loop of trav_step
+// Cooperative leaf step (round 6): the records of the waiting lanes' small leaves
+// (<= kCoopMax records, every leaf the reference's builder makes below its
+// SameNode case, bvh.rs:77) are dealt to consecutive lanes, one record per lane,
+// in rounds of <= 64 records; each leaf's lane then folds its records' results in
+// record order with the reference's update rule (bvh.rs:213-222).  A record's
+// test is a pure function of the ray and the record, so every lane's sequence of
+// `best` updates is the serial loop's.  The serial loop runs max(count) trips with
+// the waiting lanes still in them (leaf-loop lane use 0.39 on C5); a round runs
+// once per 64 records.  With the leaf batch re-tuned for it (render.h): C5 -7.7%,
+// C3 -2% at reduced spp, same images and counters (profiles/r06/variants_coop*).
+// Reached only from the 64-thread (one-wave) kernels: s_own is per block.
+constexpr uint32_t kCoopMax = 4;
+RT_D uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+template <bool ST>
+RT_D void leaf_coop(const DevBvh& B, V3 o, V3 d, Cnt<ST>& C, Trav& T) {
+    __shared__ uint8_t s_own[kWave];  // record slot -> the lane whose leaf it is
+    bool mine = T.live && T.cnt != 0 && T.cnt <= kCoopMax;
+    uint64_t todo = __ballot(mine);
+    while (todo) {
+        const uint32_t lane = stack_lane();
+        const uint32_t c = mine ? T.cnt : 0u;
+        // exclusive prefix of the record counts (c < 8: three bit planes)
+        const uint32_t p = lanes_below(__ballot(c & 1u)) + 2u * lanes_below(__ballot(c & 2u)) +
+                           4u * lanes_below(__ballot(c & 4u));
+        const bool take = mine && p + c <= (uint32_t)kWave;  // a prefix of the waiting lanes
+        const uint64_t tk = __ballot(take);
+        const uint32_t total = __builtin_amdgcn_readlane(p + c, 63 - __clzll(tk));
+        if (take) {
+            s_own[p] = (uint8_t)lane;
+            if (c > 1) s_own[p + 1] = (uint8_t)lane;
+            if (c > 2) s_own[p + 2] = (uint8_t)lane;
+            if (c > 3) s_own[p + 3] = (uint8_t)lane;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const bool item = lane < total;
+        const uint32_t own = item ? s_own[lane] : lane;
+        const uint32_t first = take ? *(const uint32_t*)(B.ctris + (size_t)T.start * kLeafBlock) : 0u;
+        const uint32_t po = __shfl(p, own), st = __shfl(T.start, own);
+        const V3 oo = v3(__shfl(o.x, own), __shfl(o.y, own), __shfl(o.z, own));
+        const V3 od = v3(__shfl(d.x, own), __shfl(d.y, own), __shfl(d.z, own));
+        double tt = -1.0, uu = 0.0, vv = 0.0;  // -1: no hit (a hit's t is >= -0 or NaN)
+        if (item) {
+            PH_COUNT(kPhLeafWave, kPhLeafLane);
+            const TriRec r = load_tri_c(B.ctris + (size_t)st * kLeafBlock + 1 + (lane - po) * kTriC);
+            double t, u = 0.0, v = 0.0;
+            if (tri_uvt_r<true>(r, oo, od, u, v, t, dir_tq(od))) { tt = t; uu = u; vv = v; }
+        }
+        int win = -1;
+        for (uint32_t k = 0; k < kCoopMax; ++k) {
+            const double x = __shfl(tt, (int)(p + k));
+            if (take && k < c && !(x < -0.5) && (!T.valid || x < T.best)) {  // update_best_intersection
+                T.valid = true; T.best = x; T.prim = first + k; T.aux = 0;
+                win = (int)(p + k);
+            }
+        }
+        const double wu = __shfl(uu, win), wv = __shfl(vv, win);
+        if (win >= 0) { T.bu = wu; T.bv = wv; }
+        if (take) { C.tri(c); mine = false; }
+        todo = __ballot(mine);
+    }
+}
+#endif
+
 // CMP: the triangle BVH's compact layout (DevBvh::cnodes / ctris, KIND 3 only):
 // the same boxes and vertices as exact f32 copies, widened to f64 before the
 // same arithmetic — every lane's visits, tests and results are the f64 form's.
@@ -295,6 +363,9 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
     bool next = false;  // this lane finished its current node and pops
     if (do_leaves) {
         const unsigned long long ph_l = PH_T();
+#ifndef RT_LEAF_SERIAL
+        if constexpr (KIND == 3 && CMP) leaf_coop(B, o, d, C, T);
+#endif
         if (T.live && T.cnt != 0) {
             if constexpr (KIND == 3) {
                 const uint32_t end = T.start + T.cnt;
@@ -312,7 +383,12 @@ RT_D void trav_step(const DevBvh& B, V3 o, V3 d, const Rcp3& rc, bool fast, Stk&
                     const float* blk = B.ctris + (size_t)T.start * kLeafBlock;
                     const uint32_t first = *(const uint32_t*)blk;
                     const bool q = dir_tq(d);
-                    for (uint32_t k = 0; k < T.cnt; ++k) {
+#ifndef RT_LEAF_SERIAL
+                    const uint32_t n_ser = T.cnt > kCoopMax ? T.cnt : 0u;  // small leaves: leaf_coop
+#else
+                    const uint32_t n_ser = T.cnt;
+#endif
+                    for (uint32_t k = 0; k < n_ser; ++k) {
                         PH_COUNT(kPhLeafWave, kPhLeafLane);
                         const TriRec cur = load_tri_c(blk + 1 + k * kTriC);
                         double t, u = 0.0, v = 0.0;

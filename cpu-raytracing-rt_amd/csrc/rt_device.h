@@ -230,7 +230,7 @@ struct Cnt {
     RT_D void lqskip() { if (ON) c.lq_skip++; }
     RT_D void segment() { if (ON) c.segments++; }
     RT_D void aabb(uint32_t n = 1) { if (ON) c.aabb += n; }
-    RT_D void tri() { if (ON) c.tri++; }
+    RT_D void tri(uint32_t n = 1) { if (ON) c.tri += n; }
     RT_D void shape() { if (ON) c.shape++; }
     RT_D void shaded() { if (ON) c.shaded++; }
     RT_D void lq() { if (ON) c.lq++; }

@@ -220,8 +220,10 @@ typedef struct rt_tuning {
                                 1 resumable triangle traversal                                          */
     uint32_t kinds;          /* 0 auto (the scene's primitive kinds); 3 the all-kinds instance; 1 or 2
                                 only as the scene's own kinds (the value rt_scene_get_tuning reports)   */
-    uint32_t suspend_lanes;  /* 0 auto (32 cache-resident BVH, 48 HBM-streamed); 1..64                   */
-    uint32_t leaf_lanes;     /* 0 auto (32 cache-resident BVH, 28 HBM-streamed); 1..64                   */
+    uint32_t suspend_lanes;  /* 0 auto (compact layouts: 24 cache-resident BVH, 48 HBM-streamed; the f64
+                                layout: 32 / 48); 1..64                                                 */
+    uint32_t leaf_lanes;     /* 0 auto (compact layouts: 16 cache-resident BVH, 12 HBM-streamed; the f64
+                                layout: 32 / 28); 1..64                                                 */
     uint32_t chunk_spp;      /* 0 the frame's rule (rt_sample_chunks); else the sample run length,
                                 raised if need be to <= 64 runs and <= 4 GiB of partial sums
                                 (rt_scene_sample_chunks reports the run length used)                    */

@@ -3,8 +3,8 @@
 — the deep, HBM-streamed BVH (the triangle BVH and its records, ~0.7 GB in the
 compact layout, are past the 256-MiB Infinity Cache).
 
-Bar: the host picks the streamed-BVH form (suspend 48, leaf batch 28, compact
-layout: api.cpp bvh_streamed), the product instance's full frame is bit-identical
+Bar: the host picks the streamed-BVH form (suspend 48, leaf batch 12 with the
+cooperative leaf step, compact layout: api.cpp bvh_streamed), the product instance's full frame is bit-identical
 to the stats instance's, and two full rows match the oracle's iterative form bit
 for bit with the device's sample chunking (bvh.rs:151-186 traversal in the
 reference's visit order; main.rs:94-111 restated, oracle rows=)."""
@@ -31,7 +31,7 @@ def test_c5_full_frame(rt, orc):
     assert info["layout_flags"] & 4  # ... with its pair layout, which the resumable kernel reads
     t = scene.tuning()
     assert (t["waves"], t["resume"], t["kinds"], t["compact"]) == (4, 1, 2, 2)
-    assert (t["suspend_lanes"], t["leaf_lanes"]) == (48, 28)  # streamed-BVH thresholds (render.h)
+    assert (t["suspend_lanes"], t["leaf_lanes"]) == (48, 12)  # streamed-BVH thresholds (render.h kLeafCoop*)
     chunks, chunk_spp = scene.sample_chunks(params)
 
     img, _, st = scene.generate_image(params, stats=True)     # stats instance

@@ -46,10 +46,13 @@ def test_fuzz_render(rt, orc, seed):
 # the compact layout's pair lines (two BVH levels per line, rt_layout.h kPairFloats) on
 # triangle-only grid scenes: ties (duplicates, shared edges and vertices, coplanar tiles),
 # flat leaf boxes and degenerate triangles through the 4-wave resumable kernel, which
-# reads the pair lines by default; the 64-B compact nodes and the eager form beside it
+# reads the pair lines by default; the 64-B compact nodes and the eager form beside it.
+# The lazy form (no suspension, leaves tested only once every live lane waits at one)
+# deals up to 256 records per leaf step: render.hip leaf_coop's multi-round case.
 PAIR_FORMS = {
     "pair": dict(resume=1, waves=4),
     "pair_eager": dict(resume=1, waves=4, suspend_lanes=64, leaf_lanes=1),
+    "pair_lazy": dict(resume=1, waves=4, suspend_lanes=1, leaf_lanes=64),
     "compact64": dict(resume=1, waves=4, compact=1),
 }
 
