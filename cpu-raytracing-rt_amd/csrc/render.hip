@@ -332,6 +332,9 @@ RT_D void leaf_coop(const DevBvh& B, V3 o, V3 d, Cnt<ST>& C, Trav& T) {
             if (tri_uvt_r<true>(r, oo, od, u, v, t, dir_tq(od))) { tt = t; uu = u; vv = v; }
         }
         int win = -1;
+        // all kCoopMax trips: bounding them by this round's largest count (a uniform
+        // trip count the compiler keeps as a loop) is +2.8% on C3 and C5
+        // (profiles/r06/variants_coopkmax_C*.log)
         for (uint32_t k = 0; k < kCoopMax; ++k) {
             const double x = __shfl(tt, (int)(p + k));
             if (take && k < c && !(x < -0.5) && (!T.valid || x < T.best)) {  // update_best_intersection
