@@ -56,8 +56,14 @@ def test_full_frame_rows_match_oracle(rt, orc, name, rows):
         # nodes, the f64 layout in the same kernel and the fused form render the identical
         # frame and counters
         assert scene.tuning()["resume"] == 1 and scene.tuning()["compact"] == 2  # pair layout
+        # the compact layouts' cooperative leaf step runs with its own thresholds (render.h
+        # kSuspendCoopCached / kLeafCoopCached); the f64 layout's serial leaf loop (and the
+        # fused form, which does not use them) reports 32 / 32
+        lanes = lambda: (scene.tuning()["suspend_lanes"], scene.tuning()["leaf_lanes"])
+        assert lanes() == (24, 16)
         for tune in (dict(compact=1), dict(compact=0), dict(resume=0)):
             scene.set_tuning(**tune)
+            assert lanes() == ((24, 16) if tune == dict(compact=1) else (32, 32)), tune  # api.cpp path_compact
             img2, _, st2 = scene.generate_image(params, stats=True)
             assert np.array_equal(img, img2), tune
             assert st2["segments"] == st["segments"] and st2["tri_tests"] == st["tri_tests"], tune
