@@ -297,7 +297,7 @@ RT_D uint32_t lanes_below(uint64_t m) {
 }
 template <bool ST>
 RT_D void leaf_coop(const DevBvh& B, V3 o, V3 d, Cnt<ST>& C, Trav& T) {
-    __shared__ uint8_t s_own[kWave];  // record slot -> the lane whose leaf it is
+    __shared__ uint8_t s_own[2 * kWave];  // record slot -> the lane whose leaf it is; [64, 128) scratch
     bool mine = T.live && T.cnt != 0 && T.cnt <= kCoopMax;
     uint64_t todo = __ballot(mine);
     while (todo) {
@@ -309,12 +309,11 @@ RT_D void leaf_coop(const DevBvh& B, V3 o, V3 d, Cnt<ST>& C, Trav& T) {
         const bool take = mine && p + c <= (uint32_t)kWave;  // a prefix of the waiting lanes
         const uint64_t tk = __ballot(take);
         const uint32_t total = __builtin_amdgcn_readlane(p + c, 63 - __clzll(tk));
-        if (take) {
-            s_own[p] = (uint8_t)lane;
-            if (c > 1) s_own[p + 1] = (uint8_t)lane;
-            if (c > 2) s_own[p + 2] = (uint8_t)lane;
-            if (c > 3) s_own[p + 3] = (uint8_t)lane;
-        }
+        // every lane writes kCoopMax bytes, the ones past its leaf into its own scratch
+        // byte: no exec-mask branches (with them, and the fold below as branches, C3 +1.1%
+        // and C5 +0.9%: profiles/r06/variants_coopbf_C*.log)
+#pragma unroll
+        for (uint32_t k = 0; k < kCoopMax; ++k) s_own[(take & (k < c)) ? p + k : kWave + lane] = (uint8_t)lane;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -331,19 +330,25 @@ RT_D void leaf_coop(const DevBvh& B, V3 o, V3 d, Cnt<ST>& C, Trav& T) {
             double t, u = 0.0, v = 0.0;
             if (tri_uvt_r<true>(r, oo, od, u, v, t, dir_tq(od))) { tt = t; uu = u; vv = v; }
         }
+        // the fold: every result fetched first, then the reference's update sequence as
+        // selects
         int win = -1;
-        // all kCoopMax trips: bounding them by this round's largest count (a uniform
-        // trip count the compiler keeps as a loop) is +2.8% on C3 and C5
-        // (profiles/r06/variants_coopkmax_C*.log)
-        for (uint32_t k = 0; k < kCoopMax; ++k) {
-            const double x = __shfl(tt, (int)(p + k));
-            if (take && k < c && !(x < -0.5) && (!T.valid || x < T.best)) {  // update_best_intersection
-                T.valid = true; T.best = x; T.prim = first + k; T.aux = 0;
-                win = (int)(p + k);
-            }
+        double x[kCoopMax];
+#pragma unroll
+        for (uint32_t k = 0; k < kCoopMax; ++k) x[k] = __shfl(tt, (int)(p + k));
+        bool valid = T.valid;
+        double best = T.best;
+        uint32_t kw = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kCoopMax; ++k) {  // update_best_intersection, by selects
+            const bool upd = take & (k < c) & !(x[k] < -0.5) & (!valid | (x[k] < best));
+            valid = valid | upd;
+            best = upd ? x[k] : best;
+            win = upd ? (int)(p + k) : win;
+            kw = upd ? k : kw;
         }
         const double wu = __shfl(uu, win), wv = __shfl(vv, win);
-        if (win >= 0) { T.bu = wu; T.bv = wv; }
+        if (win >= 0) { T.valid = true; T.best = best; T.prim = first + kw; T.aux = 0; T.bu = wu; T.bv = wv; }
         if (take) { C.tri(c); mine = false; }
         todo = __ballot(mine);
     }
