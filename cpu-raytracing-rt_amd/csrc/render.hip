@@ -289,7 +289,8 @@ RT_D TriRec load_tri_c(const float* __restrict__ p) {
 // `best` updates is the serial loop's.  The serial loop runs max(count) trips with
 // the waiting lanes still in them (leaf-loop lane use 0.39 on C5); a round runs
 // once per 64 records.  With the leaf batch re-tuned for it (render.h): C5 -7.7%,
-// C3 -2% at reduced spp, same images and counters (profiles/r06/variants_coop*).
+// C3 -2% at reduced spp, same images and counters (profiles/r06/variants_coop*); full
+// frames C3 702.3 -> 677.0 ms, C5 182.8 -> 170.7 ms (profiles/r06/bench_c*_aj.log).
 // Reached only from the 64-thread (one-wave) kernels: s_own is per block.
 constexpr uint32_t kCoopMax = 4;
 RT_D uint32_t lanes_below(uint64_t m) {
